@@ -1,0 +1,180 @@
+/*
+ * rbhip.h — C-ABI of librbhip.so, the MI355X-native (gfx950) many-body
+ * rigid-body stepper that sits behind the src/physics / src/simulation call
+ * surface of pratyay2510/RigidBody-Simulation.
+ *
+ * The reference has no FFI: every entry point below replaces a Python call
+ * site of the reference (cited per function, paths relative to the reference
+ * repository root).  The ctypes binding a maintainer would add on the
+ * reference side is shown in INTEGRATION.md; the in-tree binding is
+ * rigidbody-simulation_amd/rbhip/_lib.py.
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative errno-style code
+ *     (RB_E*); rb_last_error() returns a thread-local message for the last
+ *     failure on the calling thread.
+ *   - Host buffers are owned by the caller and never retained past a call.
+ *     Device buffers are owned by the library (a world).
+ *   - A world handle is not thread-safe: one world per host thread.
+ *   - Results are deterministic: independent of launch geometry, of the
+ *     number of ranks a scene is sharded over, and of run-to-run scheduling.
+ *   - State layout at the boundary is the reference's MuJoCo layout:
+ *     qpos stride 7 (x y z qw qx qy qz), qvel stride 6 (vx vy vz wx wy wz),
+ *     body k (0-based among free bodies) at qpos[7k], qvel[6k]
+ *     (multi_sphere_bounce.py:50-51 with the SURVEY D1 off-by-one fixed).
+ *     Inside the library the state is struct-of-arrays in HBM.
+ */
+#ifndef RBHIP_H
+#define RBHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------- */
+#define RB_OK            0
+#define RB_EINVAL      (-22)  /* bad argument / descriptor                      */
+#define RB_ENOMEM      (-12)  /* device or host allocation failed               */
+#define RB_ENODEV      (-19)  /* no HIP device / HIP runtime failure            */
+#define RB_EOVERFLOW   (-75)  /* contact or broadphase-bucket capacity exceeded */
+#define RB_EUNSUPPORTED (-95) /* box-box / box-sphere contact (not restated)    */
+#define RB_EDOM        (-33)  /* non-finite or out-of-range body position       */
+
+/* ---- enums ------------------------------------------------------------- */
+#define RB_BODY_SPHERE   0    /* size = (radius, -, -)                          */
+#define RB_BODY_BOX      1    /* size = half extents (hx, hy, hz)               */
+
+#define RB_F64           0
+#define RB_F32           1
+
+/* MuJoCo stores one normal per contact, pointing geom1 -> geom2.
+ * RAW applies it unchanged to both bodies (what collision.py:27 does);
+ * ORIENTED flips it for the body that is geom1 so it always points toward
+ * the body being solved.  Plane contacts are identical in both modes. */
+#define RB_NORMAL_ORIENTED 0
+#define RB_NORMAL_RAW      1
+
+/* contact kinds reported by rb_get_contacts */
+#define RB_CK_PLANE_SPHERE   0
+#define RB_CK_PLANE_BOX0     1   /* 1 + corner index (0..7, corner bits i&1,i&2,i&4) */
+#define RB_CK_SPHERE_SPHERE 16
+
+/* ---- scene descriptor -------------------------------------------------- */
+typedef struct rb_scene_desc {
+    int64_t n_bodies;          /* global body count N                                  */
+    int32_t n_planes;          /* <= RB_MAX_PLANES static half-spaces                   */
+    int32_t dtype;             /* RB_F64 | RB_F32 (arithmetic type of the path)        */
+    int32_t normal_convention; /* RB_NORMAL_ORIENTED | RB_NORMAL_RAW                   */
+    int32_t device;            /* HIP device ordinal                                   */
+    int32_t rank;              /* shard index: owns bodies [rank*S, rank*S+S) ∩ [0,N)  */
+    int32_t world_size;        /* shard count P; S = ceil(N / P)                       */
+    int32_t max_partners;      /* sphere-sphere contacts per body (0 = default 16)     */
+    int32_t bucket_capacity;   /* broadphase bodies per hash bucket (0 = default 16)   */
+    const int32_t *kind;       /* [N]   RB_BODY_*                                      */
+    const double  *mass;       /* [N]   model.body_mass of each free body              */
+    const double  *inertia;    /* [N*3] model.body_inertia (principal, body frame)     */
+    const double  *size;       /* [N*3] sphere: (r, 0, 0); box: half extents           */
+    const double  *planes;     /* [n_planes*6] (normal xyz, point xyz), world frame    */
+    double         gravity[3]; /* model.opt.gravity                                    */
+} rb_scene_desc;
+
+#define RB_MAX_PLANES 8
+
+typedef struct rb_world rb_world;
+
+/* ---- lifetime ---------------------------------------------------------- */
+/* Replaces the MjModel/MjData pair the reference step functions receive
+ * (collision.py:56, time_integeration.py:13, multi_sphere_bounce.py:42):
+ * masses, inertias, geometry and gravity become explicit SoA device arrays. */
+int  rb_world_create(rb_world **out, const rb_scene_desc *desc);
+void rb_world_destroy(rb_world *w);
+const char *rb_last_error(void);
+const char *rb_version(void);
+
+/* Bind the world to a caller-owned HIP stream (hipStream_t; NULL = the
+ * world's own stream).  All later work of this world is enqueued there. */
+int rb_set_stream(rb_world *w, void *hip_stream);
+
+/* ---- state transfer (the only AoS<->SoA transposes) --------------------- */
+/* Global arrays: qpos [N*7], qvel [N*6] (host).  set: every rank passes the
+ * whole scene; the world keeps all positions and its own shard of the rest.
+ * get: writes the rows of the bodies this world owns, leaves others alone.
+ * Replaces the reads/writes of data.qpos/data.qvel at collision.py:60-65,
+ * :97-100 and multi_sphere_bounce.py:50-51, :85-88. */
+int rb_set_state(rb_world *w, const double *qpos, const double *qvel);
+int rb_get_state(rb_world *w, double *qpos, double *qvel);
+/* optional data.xfrc_applied [N*6] (force xyz, torque xyz); NULL = zero
+ * (collision.py:66-67).  Host pointer, copied. */
+int rb_set_xfrc(rb_world *w, const double *xfrc);
+
+/* ---- the hot path ------------------------------------------------------ */
+/* nsteps reference steps: contact generation (mj_forward's role,
+ * collision.py:57), gravity (collision.py:66-70), the per-contact
+ * Gauss-Seidel impulse solve with Coulomb friction (collision.py:72-88 ->
+ * compute_collision_impulse_friction collision.py:7-48 ->
+ * apply_impulse_friction physics_utils.py:25-49) and the semi-implicit
+ * position/quaternion integration (collision.py:90-100).  Jacobi across
+ * bodies (one contact pass per step, multi_sphere_bounce.py:43-46).
+ * contact_threshold: contacts with |dist| < threshold are skipped
+ * (collision.py:79-80; 0 there, 1e-4 in time_integeration.py:13).
+ * Synchronous: returns after the device finished, with any device-side
+ * error (overflow, unsupported pair, non-finite position) reported. */
+int rb_step(rb_world *w, int64_t nsteps, double dt, double restitution,
+            double friction, double contact_threshold);
+/* Same, enqueued only (no host sync, no error check).  rb_sync waits and
+ * returns the accumulated device-side error. */
+int rb_step_async(rb_world *w, int64_t nsteps, double dt, double restitution,
+                  double friction, double contact_threshold);
+int rb_sync(rb_world *w);
+
+/* ---- sharded stepping (world_size > 1) ---------------------------------- */
+/* One step of the owned bodies; new owned positions land in the replicated
+ * position buffer.  The caller then all-gathers that buffer (RCCL over
+ * xGMI via torch.distributed, or any transport) and calls
+ * rb_shard_exchange_done, which publishes the other ranks' positions to the
+ * broadphase.  Both calls are enqueued only. */
+int rb_shard_step(rb_world *w, double dt, double restitution, double friction,
+                  double contact_threshold);
+int rb_shard_exchange_done(rb_world *w);
+/* Device view of the replicated position buffer: layout [P][3][S] of the
+ * world's dtype; this rank's slice is [rank][3][S] (contiguous 3*S elems). */
+int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems,
+                   int32_t *elem_bytes);
+
+/* ---- parity support ---------------------------------------------------- */
+/* Record the contact list generated during the most recent step (off by
+ * default: recording costs HBM traffic).  Canonical per-body order: plane
+ * contacts (plane order; box corners in bit order), then sphere partners by
+ * ascending body id.  Output is CSR over the owned bodies: counts[n_owned];
+ * partner (body id, or -1-plane_index), kind (RB_CK_*), dist.  cap is the
+ * capacity of the flat arrays; total receives the number of records. */
+int rb_record_contacts(rb_world *w, int enable);
+int rb_get_contacts(rb_world *w, int32_t *counts, int32_t *partner,
+                    int32_t *kind, double *dist, int64_t cap, int64_t *total);
+
+/* Known-answer entries, run as device kernels on `device`.
+ * rb_kat_impulse: per case in[24] = m, e, mu, v[3], w[3], r[3], n[3],
+ * inertia_world[9] (row-major) -> out[10] = jn, jt[3], v'[3], w'[3]:
+ * compute_collision_impulse_friction (collision.py:7-48) followed by
+ * apply_impulse_friction (physics_utils.py:25-49).  dtype RB_F64|RB_F32.
+ * rb_kat_inertia: per case in[7] = inertia_diag[3], q[4] (wxyz) ->
+ * out[18] = inertia_world[9], inv(inertia_world)[9]
+ * (compute_inertia_tensor_world collision.py:51-53 + np.linalg.inv). */
+int rb_kat_impulse(int32_t device, int32_t dtype, int64_t n, const double *in,
+                   double *out);
+int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in,
+                   double *out);
+
+/* Introspection for measurement: per-body algorithmic HBM bytes of one
+ * step (state read+write + constants), number of owned bodies, and the
+ * average device duration (ms) of the step kernel over the launches timed
+ * since the last reset (HIP events on the world's stream; enable first). */
+int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
+int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RBHIP_H */

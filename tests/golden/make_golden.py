@@ -1,0 +1,492 @@
+"""Generate the golden vectors in tests/golden/*.npz from the REFERENCE's own
+Python functions.
+
+Runs only in the build container (it needs the read-only reference checkout
+at /root/reference, which never travels to the GPU box); the .npz outputs
+are committed and are what tests read.  Usage:
+
+    python tests/golden/make_golden.py [--reference /root/reference]
+
+What is called from the reference (paths relative to its root):
+  src/physics/collision.py:7-48     compute_collision_impulse_friction
+  src/physics/physics_utils.py:25-49 apply_impulse_friction
+  src/physics/collision.py:51-53    compute_inertia_tensor_world
+  src/physics/collision.py:56-102   custom_step_with_impulse_collision_friction (C1)
+  src/physics/time_integeration.py:13-72 timestep_integration (single cube)
+
+MuJoCo is not installed here (and not installable offline), so the module
+`mujoco` those files import is pre-seeded in sys.modules with a stub that
+provides exactly what they call: mj_forward (contact generation, restated
+below in plain Python floats from MuJoCo's published plane-sphere,
+plane-box and sphere-sphere primitives — an independent restatement from
+the C oracle's), mj_name2id, mjtObj and mju_mulQuat.
+
+The N-body driver custom_step_multi_sphere (multi_sphere_bounce.py:42-92)
+cannot be imported (module-level GLFW/viewer side effects) and crashes as
+committed.  `nbody_step` below follows it line by line with D1
+(body k -> qpos[7k]) and D2 (contacts associated by body index) fixed and D8
+selectable, calling the reference's own a1/a2/a3 functions for all physics.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "rigidbody-simulation_amd"))
+from rbhip import scenes  # noqa: E402
+
+# ----------------------------------------------------------------------------
+# stub mujoco: contact generation restated in plain Python floats
+# ----------------------------------------------------------------------------
+
+
+class Contact:
+    __slots__ = ("dist", "pos", "frame", "geom1", "geom2", "body", "partner", "kind")
+
+
+def _dot3(a, b):
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]
+
+
+def _body_mat(q):
+    q = [float(v) for v in q]
+    nrm = math.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3])
+    if nrm < 1e-15:
+        q = [1.0, 0.0, 0.0, 0.0]
+    elif abs(nrm - 1.0) > 1e-15:
+        inv = 1.0 / nrm
+        q = [v * inv for v in q]
+    if q[0] == 1 and q[1] == 0 and q[2] == 0 and q[3] == 0:
+        return [1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0]
+    q00, q01, q02, q03 = q[0] * q[0], q[0] * q[1], q[0] * q[2], q[0] * q[3]
+    q11, q12, q13 = q[1] * q[1], q[1] * q[2], q[1] * q[3]
+    q22, q23, q33 = q[2] * q[2], q[2] * q[3], q[3] * q[3]
+    M = [0.0] * 9
+    M[0] = q00 + q11 - q22 - q33
+    M[4] = q00 - q11 + q22 - q33
+    M[8] = q00 - q11 - q22 + q33
+    M[1] = 2 * (q12 - q03)
+    M[2] = 2 * (q13 + q02)
+    M[3] = 2 * (q12 + q03)
+    M[5] = 2 * (q23 - q01)
+    M[6] = 2 * (q13 - q02)
+    M[7] = 2 * (q23 + q01)
+    return M
+
+
+def _mk(dist, pos, frame, g1, g2, body, partner, kind):
+    c = Contact()
+    c.dist = dist
+    c.pos = np.array(pos, dtype=np.float64)
+    c.frame = np.array(list(frame) + [0.0] * 6, dtype=np.float64)
+    c.geom1, c.geom2, c.body, c.partner, c.kind = g1, g2, body, partner, kind
+    return c
+
+
+def plane_sphere(pn, pp, c, r):
+    tmp = [c[0] - pp[0], c[1] - pp[1], c[2] - pp[2]]
+    cdist = _dot3(tmp, pn)
+    if cdist > 0.0 + r:
+        return None
+    dist = cdist - r
+    s = -dist / 2 - r
+    return dist, [c[k] + pn[k] * s for k in range(3)], list(pn)
+
+
+def plane_box(pn, pp, c, M, h):
+    dif = [c[0] - pp[0], c[1] - pp[1], c[2] - pp[2]]
+    dist = _dot3(dif, pn)
+    out = []
+    for i in range(8):
+        vec = [h[0] if i & 1 else -h[0], h[1] if i & 2 else -h[1], h[2] if i & 4 else -h[2]]
+        corner = [M[3 * k] * vec[0] + M[3 * k + 1] * vec[1] + M[3 * k + 2] * vec[2] for k in range(3)]
+        ldist = _dot3(pn, corner)
+        if dist + ldist > 0.0 or ldist > 0.0:
+            continue
+        d = dist + ldist
+        s = -d / 2
+        corner = [corner[k] + c[k] for k in range(3)]
+        out.append((i, d, [corner[k] + pn[k] * s for k in range(3)], list(pn)))
+        if len(out) >= 4:
+            break
+    return out
+
+
+def sphere_sphere(c1, r1, c2, r2):
+    dif = [c1[0] - c2[0], c1[1] - c2[1], c1[2] - c2[2]]
+    cdist = math.sqrt(_dot3(dif, dif))
+    if cdist > (0.0 + r1) + r2:
+        return None
+    dist = (cdist - r1) - r2
+    f = [c2[0] - c1[0], c2[1] - c1[1], c2[2] - c1[2]]
+    ln = math.sqrt(_dot3(f, f))
+    if ln < 1e-15:
+        f = [1.0, 0.0, 0.0]
+    else:
+        inv = 1.0 / ln
+        f = [v * inv for v in f]
+    s = r1 + dist / 2
+    return dist, [f[k] * s + c1[k] for k in range(3)], f
+
+
+class Opt:
+    def __init__(self, dt, gravity):
+        self.timestep = dt
+        self.gravity = np.array(gravity, dtype=np.float64)
+
+
+class Model:
+    """Duck-typed MjModel: the fields the reference step functions read.
+    Body ids: 0 world, 1 the static plane body, 2.. the free bodies (as in
+    models/sphere.xml and models/cube.xml)."""
+
+    def __init__(self, sc: scenes.Scene):
+        self.sc = sc
+        self.first = 2
+        nb = sc.n + self.first
+        self.body_mass = np.zeros(nb)
+        self.body_inertia = np.zeros((nb, 3))
+        self.body_mass[self.first:] = sc.mass
+        self.body_inertia[self.first:] = sc.inertia
+        self.opt = Opt(sc.dt, sc.gravity)
+        self.names = ["world", "inclined_plane"] + (sc.names or [f"b{k}" for k in range(sc.n)])
+
+
+class Data:
+    def __init__(self, model: Model):
+        sc = model.sc
+        self.qpos = sc.qpos0.reshape(-1).copy()
+        self.qvel = sc.qvel0.reshape(-1).copy()
+        self.xfrc_applied = np.zeros((sc.n + model.first, 6))
+        self.contact = []
+        self.ncon = 0
+        self.time = 0.0
+
+
+def mj_forward(model: Model, data: Data):
+    """Restated MuJoCo collision pipeline, canonical order: all plane
+    contacts by (body, plane, corner), then sphere pairs by (i, j), i < j."""
+    sc = model.sc
+    n, P = sc.n, sc.planes.shape[0]
+    pos = data.qpos.reshape(n, 7)[:, 0:3]
+    quat = data.qpos.reshape(n, 7)[:, 3:7]
+    cons = []
+    for k in range(n):
+        c = [float(v) for v in pos[k]]
+        for p in range(P):
+            pn = [float(v) for v in sc.planes[p, 0:3]]
+            pp = [float(v) for v in sc.planes[p, 3:6]]
+            if sc.kind[k] == scenes.SPHERE:
+                r = plane_sphere(pn, pp, c, float(sc.size[k, 0]))
+                if r is not None:
+                    cons.append(_mk(r[0], r[1], r[2], p, P + k, k, -1 - p, 0))
+            else:
+                M = _body_mat(quat[k])
+                for (corner, d, cp, fr) in plane_box(pn, pp, c, M, [float(v) for v in sc.size[k]]):
+                    cons.append(_mk(d, cp, fr, p, P + k, k, -1 - p, 1 + corner))
+    sph = np.where(sc.kind == scenes.SPHERE)[0]
+    if len(sph) > 1:
+        ps = pos[sph]
+        d2 = ((ps[:, None, :] - ps[None, :, :]) ** 2).sum(-1)
+        rad = sc.size[sph, 0]
+        lim = (rad[:, None] + rad[None, :]) * 1.001 + 1e-12
+        ii, jj = np.nonzero(np.triu(d2 <= lim * lim, 1))
+        for a, b in zip(ii, jj):
+            i, j = int(sph[a]), int(sph[b])
+            r = sphere_sphere([float(v) for v in pos[i]], float(sc.size[i, 0]),
+                              [float(v) for v in pos[j]], float(sc.size[j, 0]))
+            if r is not None:
+                cons.append(_mk(r[0], r[1], r[2], P + i, P + j, (i, j), (i, j), 16))
+    boxes = np.where(sc.kind == scenes.BOX)[0]
+    if len(boxes):
+        bound = np.where(sc.kind == scenes.BOX, np.linalg.norm(sc.size, axis=1), sc.size[:, 0])
+        d = np.linalg.norm(pos[:, None, :] - pos[None, :, :], axis=-1)
+        hit = np.triu(d <= bound[:, None] + bound[None, :], 1)
+        hit &= (sc.kind[:, None] == scenes.BOX) | (sc.kind[None, :] == scenes.BOX)
+        assert not hit.any(), "box-involved pair in contact: not restated"
+    data.contact = cons
+    data.ncon = len(cons)
+
+
+def mj_name2id(model, objtype, name):
+    try:
+        return model.names.index(name)
+    except ValueError:
+        return -1
+
+
+def mju_mulQuat(res, a, b):
+    a = [float(v) for v in a]
+    b = [float(v) for v in b]
+    res[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3]
+    res[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2]
+    res[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1]
+    res[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]
+
+
+def install_stub():
+    mj = types.ModuleType("mujoco")
+    mj.mj_forward = mj_forward
+    mj.mj_name2id = mj_name2id
+    mj.mju_mulQuat = mju_mulQuat
+    mj.mjtObj = types.SimpleNamespace(mjOBJ_BODY=1)
+    sys.modules["mujoco"] = mj
+
+
+# ----------------------------------------------------------------------------
+# N-body driver: multi_sphere_bounce.py:42-92 with D1/D2 fixed, D8 selectable
+# ----------------------------------------------------------------------------
+
+def nbody_step(ref, model: Model, data: Data, dt, restitution, friction, threshold=0.0,
+               normal_convention="oriented"):
+    mj_forward(model, data)                                           # :43
+    n = model.sc.n
+    per_body = [[] for _ in range(n)]
+    for c in data.contact:                                            # D2: by body index
+        if isinstance(c.body, tuple):
+            per_body[c.body[0]].append(c)
+            per_body[c.body[1]].append(c)
+        else:
+            per_body[c.body].append(c)
+    for k in range(n):                                                # :46
+        body_id = model.first + k
+        mass = model.body_mass[body_id]                               # :48
+        inertia_diag = model.body_inertia[body_id]
+        qpos = data.qpos[k * 7: k * 7 + 7]                            # :50 (D1 fixed)
+        qvel = data.qvel[k * 6: k * 6 + 6]
+        vel = qvel[:3]
+        omega = qvel[3:6]
+        inertia_world = ref.compute_inertia_tensor_world(inertia_diag, qpos[3:7])   # :55
+        force = data.xfrc_applied[body_id, :3] + mass * model.opt.gravity           # :58
+        torque = data.xfrc_applied[body_id, 3:]
+        vel += (force / mass) * dt                                                  # :60
+        omega += np.linalg.inv(inertia_world) @ (torque * dt)
+        for contact in per_body[k]:                                   # :64
+            if not np.isnan(contact.dist) and contact.dist < 0:       # time_integeration.py:46
+                if abs(contact.dist) < threshold:                     # time_integeration.py:50
+                    continue
+                contact_point = contact.pos - qpos[:3]                # :67
+                normal = contact.frame[:3]                            # :68
+                if (normal_convention == "oriented" and isinstance(contact.partner, tuple)
+                        and contact.partner[0] == k):                 # D8: body is geom1
+                    normal = -normal
+                jn, jt = ref.compute_collision_impulse_friction(
+                    mass, inertia_world, vel, omega, contact_point, normal, restitution, friction)
+                vel, omega = ref.apply_impulse_friction(
+                    vel, omega, mass, inertia_world, contact_point, normal, jn, jt)
+        pos_new = qpos[:3] + vel * dt                                 # :77
+        omega_quat = np.concatenate([[0], omega])
+        res = np.zeros(4)
+        mju_mulQuat(res, omega_quat, qpos[3:7])
+        quat_new = qpos[3:7] + 0.5 * res * dt
+        quat_new /= np.linalg.norm(quat_new)
+        data.qpos[k * 7: k * 7 + 3] = pos_new                         # :85
+        data.qpos[k * 7 + 3: k * 7 + 7] = quat_new
+        data.qvel[k * 6: k * 6 + 3] = vel
+        data.qvel[k * 6 + 3: k * 6 + 6] = omega
+
+
+def contact_table(data: Data, n: int):
+    """Per-body canonical lists (planes, then partners ascending) as CSR."""
+    per = [[] for _ in range(n)]
+    for c in data.contact:
+        if isinstance(c.body, tuple):
+            i, j = c.body
+            per[i].append((j, 16, c.dist))
+            per[j].append((i, 16, c.dist))
+        else:
+            per[c.body].append((c.partner, c.kind, c.dist))
+    for k in range(n):
+        planes = [t for t in per[k] if t[0] < 0]
+        pairs = sorted([t for t in per[k] if t[0] >= 0], key=lambda t: t[0])
+        per[k] = planes + pairs
+    counts = np.array([len(p) for p in per], np.int32)
+    flat = [t for p in per for t in p]
+    partner = np.array([t[0] for t in flat], np.int32)
+    kind = np.array([t[1] for t in flat], np.int32)
+    dist = np.array([t[2] for t in flat], np.float64)
+    return counts, partner, kind, dist
+
+
+# ----------------------------------------------------------------------------
+# generators
+# ----------------------------------------------------------------------------
+
+def gen_kat_impulse(ref, rng, n_random=2000):
+    """a1+a2 known answers: random cases + the edge cases SURVEY §4 lists."""
+    from scipy.spatial.transform import Rotation as R  # noqa: F401  (reference dependency)
+    rows = []
+
+    def case(m, e, mu, v, w, r, nrm, Iw):
+        rows.append(np.concatenate([[m, e, mu], v, w, r, nrm, np.asarray(Iw).reshape(9)]))
+
+    for t in range(n_random):
+        m = rng.uniform(0.05, 30.0)
+        q = rng.standard_normal(4)
+        if t % 3 == 0:
+            Id = np.full(3, rng.uniform(1e-4, 3.0))                     # isotropic (all scenes)
+        else:
+            Id = rng.uniform(1e-3, 3.0, 3)                              # anisotropic
+        Iw = ref.compute_inertia_tensor_world(Id, q)
+        nrm = rng.standard_normal(3)
+        nrm /= np.linalg.norm(nrm)
+        v = rng.normal(0, 2.0, 3)
+        w = rng.normal(0, 3.0, 3)
+        r = rng.normal(0, 0.3, 3)
+        e = [0.0, 1.0, rng.uniform(0, 1)][t % 3]
+        mu = [0.0, rng.uniform(0, 1.5), 0.3][(t // 3) % 3]
+        case(m, e, mu, v, w, r, nrm, Iw)
+    I1 = ref.compute_inertia_tensor_world(np.full(3, 0.02), np.array([1.0, 0, 0, 0]))
+    z = np.array([0.0, 0.0, 1.0])
+    # u_n == 0 exactly (returns zeros): n = z, u_z = 0
+    case(1.0, 0.8, 0.3, np.array([0.3, -0.2, 0.0]), np.array([0.0, 0.0, 1.5]),
+         np.array([0.1, 0.2, -0.1]), z, I1)
+    # separating
+    case(1.0, 0.8, 0.3, np.array([0.3, -0.2, 0.5]), np.zeros(3), np.array([0, 0, -0.1]), z, I1)
+    # |u_t| exactly 1e-6 (no friction), just below and just above
+    for ut in (1e-6, np.nextafter(1e-6, 0), np.nextafter(1e-6, 1)):
+        case(1.0, 0.5, 0.3, np.array([ut, 0.0, -1.0]), np.zeros(3), np.array([0, 0, -0.1]), z, I1)
+    # friction cap binding / not binding, mu = 0, e = 0, e = 1
+    for (e, mu) in ((0.0, 0.3), (1.0, 0.3), (0.8, 0.0), (0.8, 5.0), (0.8, 1e-3)):
+        case(0.7, e, mu, np.array([0.4, -0.3, -2.0]), np.array([1.0, 2.0, -0.5]),
+             np.array([0.05, -0.02, -0.1]), z, I1)
+    inp = np.array(rows)
+    out = np.zeros((len(rows), 10))
+    for i, row in enumerate(inp):
+        m, e, mu = row[0], row[1], row[2]
+        v, w, r, nrm = row[3:6], row[6:9], row[9:12], row[12:15]
+        Iw = row[15:24].reshape(3, 3)
+        jn, jt = ref.compute_collision_impulse_friction(m, Iw, v, w, r, nrm, e, mu)
+        v2, w2 = ref.apply_impulse_friction(v, w, m, Iw, r, nrm, jn, jt)
+        out[i] = np.concatenate([[jn], jt, v2, w2])
+    return inp, out
+
+
+def gen_kat_inertia(ref, rng, n=1000):
+    inp = np.zeros((n, 7))
+    out = np.zeros((n, 18))
+    for i in range(n):
+        Id = np.full(3, rng.uniform(1e-4, 3.0)) if i % 2 == 0 else rng.uniform(1e-3, 3.0, 3)
+        q = rng.standard_normal(4) * rng.uniform(0.5, 2.0)
+        if i % 5 == 0:
+            q = q / np.linalg.norm(q)
+        inp[i, 0:3], inp[i, 3:7] = Id, q
+        Iw = ref.compute_inertia_tensor_world(Id, q)
+        out[i, 0:9] = Iw.reshape(9)
+        out[i, 9:18] = np.linalg.inv(Iw).reshape(9)
+    return inp, out
+
+
+def run_single(ref_step, sc: scenes.Scene, obj: str, steps: int, **kw):
+    install_stub()
+    model = Model(sc)
+    data = Data(model)
+    qpos = np.zeros((steps + 1, 7))
+    qvel = np.zeros((steps + 1, 6))
+    ncon = np.zeros(steps, np.int32)
+    qpos[0], qvel[0] = data.qpos, data.qvel
+    for t in range(steps):
+        ref_step(model, obj, data, dt=model.opt.timestep, **kw)
+        ncon[t] = data.ncon
+        qpos[t + 1], qvel[t + 1] = data.qpos, data.qvel
+    return qpos, qvel, ncon
+
+
+def run_nbody(ref, sc: scenes.Scene, steps: int, every: int, contact_steps: int):
+    model = Model(sc)
+    data = Data(model)
+    snaps_q, snaps_v, snap_t = [sc.qpos0.copy()], [sc.qvel0.copy()], [0]
+    c_counts, c_partner, c_kind, c_dist, c_off = [], [], [], [], [0]
+    for t in range(steps):
+        nbody_step(ref, model, data, sc.dt, sc.restitution, sc.friction, sc.threshold,
+                   sc.normal_convention)
+        if t < contact_steps:
+            cnt, par, kin, dis = contact_table(data, sc.n)
+            c_counts.append(cnt)
+            c_partner.append(par)
+            c_kind.append(kin)
+            c_dist.append(dis)
+            c_off.append(c_off[-1] + len(par))
+        if (t + 1) % every == 0 or t + 1 == steps:
+            snaps_q.append(data.qpos.reshape(sc.n, 7).copy())
+            snaps_v.append(data.qvel.reshape(sc.n, 6).copy())
+            snap_t.append(t + 1)
+    return dict(snap_step=np.array(snap_t), qpos=np.array(snaps_q), qvel=np.array(snaps_v),
+                c_counts=np.array(c_counts), c_off=np.array(c_off, np.int64),
+                c_partner=np.concatenate(c_partner) if c_partner else np.zeros(0, np.int32),
+                c_kind=np.concatenate(c_kind) if c_kind else np.zeros(0, np.int32),
+                c_dist=np.concatenate(c_dist) if c_dist else np.zeros(0))
+
+
+def scene_arrays(sc: scenes.Scene):
+    return dict(kind=sc.kind, mass=sc.mass, inertia=sc.inertia, size=sc.size, planes=sc.planes,
+                gravity=sc.gravity, qpos0=sc.qpos0, qvel0=sc.qvel0,
+                params=np.array([sc.dt, sc.restitution, sc.friction, sc.threshold]),
+                normal_raw=np.array(sc.normal_convention == "raw"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    install_stub()
+    sys.path.insert(0, args.reference)
+    from src.physics import collision as ref_collision
+    from src.physics import physics_utils as ref_utils
+    from src.physics import time_integeration as ref_ti
+
+    class Ref:
+        compute_collision_impulse_friction = staticmethod(ref_collision.compute_collision_impulse_friction)
+        apply_impulse_friction = staticmethod(ref_utils.apply_impulse_friction)
+        compute_inertia_tensor_world = staticmethod(ref_collision.compute_inertia_tensor_world)
+
+    ref = Ref()
+    only = set(args.only.split(",")) if args.only else None
+
+    def want(name):
+        return only is None or name in only
+
+    out = lambda name, **kw: np.savez_compressed(os.path.join(HERE, name + ".npz"), **kw)  # noqa: E731
+    rng = np.random.default_rng(20250614)
+    if want("kat_impulse"):
+        inp, res = gen_kat_impulse(ref, rng)
+        out("kat_impulse", inp=inp, out=res)
+    if want("kat_inertia"):
+        inp, res = gen_kat_inertia(ref, rng)
+        out("kat_inertia", inp=inp, out=res)
+    if want("traj_single_sphere"):
+        # C1: single_sphere_bounce.py:65-69 passes obj "sphere" (SURVEY D4:
+        # mj_name2id -> -1 -> the last body, the ball) and the config's e, mu.
+        sc = scenes.single_sphere()
+        q, v, ncon = run_single(ref_collision.custom_step_with_impulse_collision_friction, sc,
+                                "sphere", 2000, restitution=sc.restitution, friction_coeff=sc.friction)
+        out("traj_single_sphere", qpos=q, qvel=v, ncon=ncon, **scene_arrays(sc))
+    if want("traj_single_cube"):
+        sc = scenes.single_cube()
+        q, v, ncon = run_single(ref_ti.timestep_integration, sc, "cube", 2000,
+                                restitution=sc.restitution, friction_coeff=sc.friction)
+        out("traj_single_cube", qpos=q, qvel=v, ncon=ncon, **scene_arrays(sc))
+    nb = [
+        ("traj_multi4", scenes.multi_sphere4(), 400, 10, 400),
+        ("traj_flat64", scenes.flat_spheres(8, 8, seed=0), 200, 10, 200),
+        ("traj_flat64_raw", scenes.flat_spheres(8, 8, seed=1).with_(normal_convention="raw"), 120, 10, 120),
+        ("traj_flat256", scenes.flat_spheres(16, 16, seed=2), 150, 10, 150),
+        ("traj_incline64", scenes.incline_spheres(8, 8, seed=3), 200, 10, 200),
+        ("traj_cubes16", scenes.incline_cubes(4, 4, seed=4), 240, 10, 240),
+    ]
+    for name, sc, steps, every, csteps in nb:
+        if want(name):
+            res = run_nbody(ref, sc, steps, every, csteps)
+            out(name, **res, **scene_arrays(sc))
+            print(name, "done", res["c_partner"].shape)
+
+
+if __name__ == "__main__":
+    main()
