@@ -166,6 +166,11 @@ int rb_kat_impulse(int32_t device, int32_t dtype, int64_t n, const double *in,
                    double *out);
 int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in,
                    double *out);
+/* rb_kat_apply: apply_impulse_friction alone (physics_utils.py:25-49) with
+ * caller-given impulses: in[26] = m, v[3], w[3], r[3], n[3], jn, jt[3],
+ * inertia_world[9] -> out[6] = v'[3], w'[3]. */
+int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in,
+                 double *out);
 
 /* Introspection for measurement: per-body algorithmic HBM bytes of one
  * step (state read+write + constants), number of owned bodies, and the

@@ -1,0 +1,672 @@
+// rb_capi.hip — implementation of include/rbhip.h.
+//
+// A world owns its device buffers (struct-of-arrays state, replicated
+// constants, three rotating broadphase tables) and enqueues all work on one
+// HIP stream.  Multi-step calls on a single shard are captured once into a
+// hipGraph (one kernel node per step) and replayed, so K steps cost one host
+// submission.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/rbhip.h"
+#include "rb_internal.hpp"
+
+using namespace rb;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(e_ == hipErrorOutOfMemory ? RB_ENOMEM : RB_ENODEV, "%s: %s (%s:%d)", #expr, \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                           \
+    } while (0)
+
+int64_t next_pow2(int64_t v) {
+    int64_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+int err_to_code(int32_t bits) {
+    if (bits & ERR_DOMAIN) return fail(RB_EDOM, "device: non-finite or out-of-range body position");
+    if (bits & ERR_UNSUPPORTED)
+        return fail(RB_EUNSUPPORTED, "device: box-box / box-sphere pair within contact range (not restated)");
+    if (bits & ERR_PARTNER_OVERFLOW) return fail(RB_EOVERFLOW, "device: a body has more sphere partners than max_partners");
+    if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: broadphase bucket capacity exceeded");
+    return RB_OK;
+}
+
+}  // namespace
+
+struct rb_world {
+    int dtype = RB_F64, esz = 8, device = 0;
+    hipStream_t stream = nullptr, own_stream = nullptr, cap_stream = nullptr;
+    int64_t N = 0, S = 0, Npad = 0, lo = 0;
+    int32_t n_local = 0, P = 1, rank = 0;
+    int32_t n_planes = 0, oriented = 1, maxp = 16, cap = 16, maxrec = 0;
+    double planes[RB_MAX_PLANES][6] = {};
+    double g[3] = {};
+    double inv_cs = 1.0;
+    int64_t H = 1024;
+    int64_t bytes_per_body_step = 0;
+    // device memory
+    void *gpos = nullptr;      // [P][3][S]
+    void *state = nullptr;     // 10 x S  (qw qx qy qz vx vy vz wx wy wz)
+    void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
+    int32_t *kind = nullptr;   // Npad
+    void *xfrc = nullptr;      // 6 x S or null
+    int32_t *cnt[3] = {};
+    void *ent[3] = {};
+    int32_t *err = nullptr;
+    int32_t *err_host = nullptr;   // pinned
+    // recording
+    bool record = false;
+    int32_t *rec_count = nullptr, *rec_partner = nullptr, *rec_kind = nullptr;
+    void *rec_dist = nullptr;
+    // stepping state
+    int phase = 0;
+    bool primed = false;
+    std::map<std::tuple<int64_t, int, double, double, double, double, int>, hipGraphExec_t> graphs;
+    // kernel timing
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+    double t_sum_ms = 0;
+    int64_t t_n = 0;
+};
+
+namespace {
+
+template <typename T> T *dp(void *p, int64_t off) { return reinterpret_cast<T *>(p) + off; }
+
+template <typename T> StepParams<T> make_step(rb_world *w, double dt, double e, double mu, double thr) {
+    StepParams<T> p{};
+    p.n_global = w->N;
+    p.n_local = w->n_local;
+    p.lo = (int32_t)w->lo;
+    p.S = (int32_t)w->S;
+    T *gp = dp<T>(w->gpos, (int64_t)w->rank * 3 * w->S);
+    p.st.px = gp; p.st.py = gp + w->S; p.st.pz = gp + 2 * w->S;
+    T *st = dp<T>(w->state, 0);
+    T **f[10] = {&p.st.qw, &p.st.qx, &p.st.qy, &p.st.qz, &p.st.vx, &p.st.vy, &p.st.vz, &p.st.wx, &p.st.wy, &p.st.wz};
+    for (int k = 0; k < 10; ++k) *f[k] = st + k * w->S;
+    const T *c = dp<T>(w->consts, 0);
+    p.cs.mass = c; p.cs.ix = c + w->Npad; p.cs.iy = c + 2 * w->Npad; p.cs.iz = c + 3 * w->Npad;
+    p.cs.sx = c + 4 * w->Npad; p.cs.sy = c + 5 * w->Npad; p.cs.sz = c + 6 * w->Npad;
+    p.cs.bound = c + 7 * w->Npad;
+    p.cs.kind = w->kind;
+    p.xfrc = w->xfrc ? dp<T>(w->xfrc, 0) : nullptr;
+    p.n_planes = w->n_planes;
+    for (int k = 0; k < w->n_planes; ++k)
+        for (int d = 0; d < 3; ++d) { p.pn[k][d] = (T)w->planes[k][d]; p.pp[k][d] = (T)w->planes[k][3 + d]; }
+    for (int d = 0; d < 3; ++d) p.g[d] = (T)w->g[d];
+    p.dt = (T)dt; p.e = (T)e; p.mu = (T)mu; p.thr = (T)thr;
+    p.oriented = w->oriented;
+    p.grid.inv_cs = (T)w->inv_cs;
+    p.grid.hmask = (uint32_t)(w->H - 1);
+    p.grid.cap = w->cap;
+    p.grid.H = (int32_t)w->H;
+    p.err = w->err;
+    if (w->record) {
+        p.rec_count = w->rec_count; p.rec_partner = w->rec_partner; p.rec_kind = w->rec_kind;
+        p.rec_dist = dp<T>(w->rec_dist, 0);
+        p.maxrec = w->maxrec;
+    }
+    return p;
+}
+
+template <typename T> void set_tables(rb_world *w, StepParams<T> &p, int ph) {
+    p.cnt_cur = w->cnt[ph];
+    p.ent_cur = dp<Entry<T>>(w->ent[ph], 0);
+    p.cnt_next = w->cnt[(ph + 1) % 3];
+    p.ent_next = dp<Entry<T>>(w->ent[(ph + 1) % 3], 0);
+    p.cnt_clear = w->cnt[(ph + 2) % 3];
+}
+
+template <typename T> InsertParams<T> make_insert(rb_world *w, int ph, int64_t first, int64_t count,
+                                                  int64_t skip_lo, int64_t skip_hi) {
+    InsertParams<T> ip{};
+    ip.gpos = dp<T>(w->gpos, 0);
+    ip.S = (int32_t)w->S;
+    ip.first = first; ip.count = count; ip.skip_lo = skip_lo; ip.skip_hi = skip_hi;
+    ip.grid.inv_cs = (T)w->inv_cs;
+    ip.grid.hmask = (uint32_t)(w->H - 1);
+    ip.grid.cap = w->cap;
+    ip.grid.H = (int32_t)w->H;
+    ip.cnt = w->cnt[ph];
+    ip.ent = dp<Entry<T>>(w->ent[ph], 0);
+    ip.err = w->err;
+    return ip;
+}
+
+// (re)build the current table from every body's position
+int prime(rb_world *w) {
+    for (int k = 0; k < 3; ++k) HIPCHK(hipMemsetAsync(w->cnt[k], 0, sizeof(int32_t) * w->H, w->stream));
+    hipError_t e = w->dtype == RB_F64
+                       ? launch_insert<double>(make_insert<double>(w, w->phase, 0, w->N, 0, 0), w->stream)
+                       : launch_insert<float>(make_insert<float>(w, w->phase, 0, w->N, 0, 0), w->stream);
+    HIPCHK(e);
+    w->primed = true;
+    return RB_OK;
+}
+
+int launch_one(rb_world *w, hipStream_t s, int ph, double dt, double e, double mu, double thr, bool insert_next) {
+    hipError_t r;
+    if (w->dtype == RB_F64) {
+        StepParams<double> p = make_step<double>(w, dt, e, mu, thr);
+        set_tables(w, p, ph);
+        if (!insert_next) { p.cnt_next = nullptr; p.ent_next = nullptr; }
+        r = launch_step<double>(p, w->maxp, s);
+    } else {
+        StepParams<float> p = make_step<float>(w, dt, e, mu, thr);
+        set_tables(w, p, ph);
+        if (!insert_next) { p.cnt_next = nullptr; p.ent_next = nullptr; }
+        r = launch_step<float>(p, w->maxp, s);
+    }
+    HIPCHK(r);
+    return RB_OK;
+}
+
+int read_err(rb_world *w) {
+    HIPCHK(hipMemcpyAsync(w->err_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const int32_t bits = *w->err_host;
+    if (bits) {
+        HIPCHK(hipMemsetAsync(w->err, 0, sizeof(int32_t), w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        return err_to_code(bits);
+    }
+    return RB_OK;
+}
+
+int collect_timing(rb_world *w) {
+    if (w->tev.empty()) return RB_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    for (auto &pr : w->tev) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+        w->t_sum_ms += ms;
+        w->t_n += 1;
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    w->tev.clear();
+    return RB_OK;
+}
+
+int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
+    if (w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_step + exchange");
+    if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0))
+        return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
+    if (nsteps == 0) return RB_OK;
+    hipError_t se = hipSetDevice(w->device);
+    HIPCHK(se);
+    if (!w->primed) { int rc = prime(w); if (rc) return rc; }
+    if (w->timing) {
+        // eager launches, each bracketed by events on the launch stream
+        for (int64_t k = 0; k < nsteps; ++k) {
+            hipEvent_t a, b;
+            HIPCHK(hipEventCreate(&a));
+            HIPCHK(hipEventCreate(&b));
+            HIPCHK(hipEventRecord(a, w->stream));
+            int rc = launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(b, w->stream));
+            w->tev.emplace_back(a, b);
+            w->phase = (w->phase + 1) % 3;
+            if (w->tev.size() >= 4096) { int rc2 = collect_timing(w); if (rc2) return rc2; }
+        }
+        return RB_OK;
+    }
+    if (nsteps == 1) {
+        int rc = launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+        if (rc) return rc;
+        w->phase = (w->phase + 1) % 3;
+        return RB_OK;
+    }
+    // K > 1: replay a captured graph of K step nodes
+    const int64_t chunk_max = 512;
+    int64_t left = nsteps;
+    while (left > 0) {
+        const int64_t K = left > chunk_max ? chunk_max : left;
+        auto key = std::make_tuple(K, w->phase, dt, e, mu, thr, (int)w->record);
+        auto it = w->graphs.find(key);
+        if (it == w->graphs.end()) {
+            if (w->graphs.size() >= 30) {
+                for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+                w->graphs.clear();
+            }
+            // capture the three table-phase variants at once, so later calls
+            // starting at any phase replay without a capture
+            for (int ph0 = 0; ph0 < 3; ++ph0) {
+                hipGraph_t graph;
+                hipGraphExec_t ex;
+                HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
+                int ph = ph0;
+                for (int64_t k = 0; k < K; ++k) {
+                    int rc = launch_one(w, w->cap_stream, ph, dt, e, mu, thr, true);
+                    if (rc) { (void)hipStreamEndCapture(w->cap_stream, &graph); return rc; }
+                    ph = (ph + 1) % 3;
+                }
+                HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
+                HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(graph);
+                w->graphs[std::make_tuple(K, ph0, dt, e, mu, thr, (int)w->record)] = ex;
+            }
+            it = w->graphs.find(key);
+        }
+        hipGraphExec_t exec = it->second;
+        HIPCHK(hipGraphLaunch(exec, w->stream));
+        w->phase = (int)((w->phase + K) % 3);
+        left -= K;
+    }
+    return RB_OK;
+}
+
+template <typename T>
+int upload_state(rb_world *w, const double *qpos, const double *qvel) {
+    std::vector<T> g((size_t)w->P * 3 * w->S, T(0));
+    for (int64_t b = 0; b < w->N; ++b) {
+        const int64_t r = b / w->S, l = b % w->S;
+        for (int d = 0; d < 3; ++d) g[(size_t)(r * 3 * w->S + d * w->S + l)] = (T)qpos[7 * b + d];
+    }
+    std::vector<T> st((size_t)10 * w->S, T(0));
+    for (int64_t l = 0; l < w->n_local; ++l) {
+        const int64_t b = w->lo + l;
+        for (int d = 0; d < 4; ++d) st[(size_t)(d * w->S + l)] = (T)qpos[7 * b + 3 + d];
+        for (int d = 0; d < 6; ++d) st[(size_t)((4 + d) * w->S + l)] = (T)qvel[6 * b + d];
+    }
+    HIPCHK(hipMemcpyAsync(w->gpos, g.data(), sizeof(T) * g.size(), hipMemcpyHostToDevice, w->stream));
+    HIPCHK(hipMemcpyAsync(w->state, st.data(), sizeof(T) * st.size(), hipMemcpyHostToDevice, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return RB_OK;
+}
+
+template <typename T>
+int download_state(rb_world *w, double *qpos, double *qvel) {
+    std::vector<T> g((size_t)3 * w->S), st((size_t)10 * w->S);
+    HIPCHK(hipMemcpyAsync(g.data(), dp<T>(w->gpos, (int64_t)w->rank * 3 * w->S), sizeof(T) * g.size(),
+                          hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipMemcpyAsync(st.data(), w->state, sizeof(T) * st.size(), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    for (int64_t l = 0; l < w->n_local; ++l) {
+        const int64_t b = w->lo + l;
+        if (qpos) {
+            for (int d = 0; d < 3; ++d) qpos[7 * b + d] = (double)g[(size_t)(d * w->S + l)];
+            for (int d = 0; d < 4; ++d) qpos[7 * b + 3 + d] = (double)st[(size_t)(d * w->S + l)];
+        }
+        if (qvel)
+            for (int d = 0; d < 6; ++d) qvel[6 * b + d] = (double)st[(size_t)((4 + d) * w->S + l)];
+    }
+    return RB_OK;
+}
+
+template <typename T>
+int upload_consts(rb_world *w, const rb_scene_desc *d) {
+    std::vector<T> c((size_t)8 * w->Npad, T(0));
+    double rmax = 0;
+    for (int64_t b = 0; b < w->N; ++b) {
+        const double *s = d->size + 3 * b;
+        const double bound = d->kind[b] == RB_BODY_SPHERE ? s[0] : sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+        if (bound > rmax) rmax = bound;
+        c[(size_t)(0 * w->Npad + b)] = (T)d->mass[b];
+        for (int k = 0; k < 3; ++k) {
+            c[(size_t)((1 + k) * w->Npad + b)] = (T)d->inertia[3 * b + k];
+            c[(size_t)((4 + k) * w->Npad + b)] = (T)s[k];
+        }
+        c[(size_t)(7 * w->Npad + b)] = (T)bound;
+    }
+    const double cs = rmax > 0 ? 2.0 * rmax * 1.001 : 1.0;
+    w->inv_cs = 1.0 / cs;
+    HIPCHK(hipMemcpy(w->consts, c.data(), sizeof(T) * c.size(), hipMemcpyHostToDevice));
+    std::vector<int32_t> k((size_t)w->Npad, 0);
+    for (int64_t b = 0; b < w->N; ++b) k[(size_t)b] = d->kind[b];
+    HIPCHK(hipMemcpy(w->kind, k.data(), sizeof(int32_t) * k.size(), hipMemcpyHostToDevice));
+    return RB_OK;
+}
+
+void free_world(rb_world *w) {
+    if (!w) return;
+    (void)hipSetDevice(w->device);
+    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    void *bufs[] = {w->gpos, w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
+                    w->ent[0], w->ent[1], w->ent[2], w->err, w->rec_count, w->rec_partner, w->rec_kind,
+                    w->rec_dist};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (w->err_host) (void)hipHostFree(w->err_host);
+    if (w->own_stream) (void)hipStreamDestroy(w->own_stream);
+    if (w->cap_stream) (void)hipStreamDestroy(w->cap_stream);
+    delete w;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rb_last_error(void) { return g_err.c_str(); }
+const char *rb_version(void) { return "librbhip 0.1 (gfx950, HIP)"; }
+
+int rb_world_create(rb_world **out, const rb_scene_desc *d) {
+    if (!out || !d) return fail(RB_EINVAL, "null argument");
+    *out = nullptr;
+    if (d->n_bodies <= 0 || d->n_bodies > (int64_t)INT32_MAX / 2) return fail(RB_EINVAL, "n_bodies out of range");
+    if (d->n_planes < 0 || d->n_planes > RB_MAX_PLANES) return fail(RB_EINVAL, "n_planes must be in [0, %d]", RB_MAX_PLANES);
+    if (d->dtype != RB_F64 && d->dtype != RB_F32) return fail(RB_EINVAL, "dtype must be RB_F64 or RB_F32");
+    if (d->world_size < 1 || d->rank < 0 || d->rank >= d->world_size) return fail(RB_EINVAL, "bad rank/world_size");
+    if (!d->kind || !d->mass || !d->inertia || !d->size || (d->n_planes && !d->planes))
+        return fail(RB_EINVAL, "null scene array");
+    if (d->normal_convention != RB_NORMAL_ORIENTED && d->normal_convention != RB_NORMAL_RAW)
+        return fail(RB_EINVAL, "bad normal_convention");
+    const int maxp = d->max_partners > 0 ? d->max_partners : 16;
+    if (maxp > 32) return fail(RB_EINVAL, "max_partners must be <= 32");
+    for (int64_t b = 0; b < d->n_bodies; ++b) {
+        if (d->kind[b] != RB_BODY_SPHERE && d->kind[b] != RB_BODY_BOX) return fail(RB_EINVAL, "body %lld: bad kind", (long long)b);
+        if (!(d->mass[b] > 0)) return fail(RB_EINVAL, "body %lld: mass must be > 0", (long long)b);
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RB_ENODEV, "no HIP device available");
+    if (d->device < 0 || d->device >= ndev) return fail(RB_ENODEV, "device %d out of range (have %d)", d->device, ndev);
+
+    rb_world *w = new rb_world();
+    w->dtype = d->dtype;
+    w->esz = d->dtype == RB_F64 ? 8 : 4;
+    w->device = d->device;
+    w->N = d->n_bodies;
+    w->P = d->world_size;
+    w->rank = d->rank;
+    w->S = (w->N + w->P - 1) / w->P;
+    w->Npad = w->S * w->P;
+    w->lo = w->S * w->rank;
+    const int64_t hi = w->lo + w->S < w->N ? w->lo + w->S : w->N;
+    w->n_local = (int32_t)(hi > w->lo ? hi - w->lo : 0);
+    w->n_planes = d->n_planes;
+    for (int k = 0; k < d->n_planes; ++k)
+        for (int j = 0; j < 6; ++j) w->planes[k][j] = d->planes[6 * k + j];
+    for (int j = 0; j < 3; ++j) w->g[j] = d->gravity[j];
+    w->oriented = d->normal_convention == RB_NORMAL_ORIENTED;
+    w->maxp = maxp;
+    w->cap = d->bucket_capacity > 0 ? d->bucket_capacity : 16;
+    w->maxrec = 4 * w->n_planes + w->maxp;
+    w->H = next_pow2(2 * w->N > 1024 ? 2 * w->N : 1024);
+    int64_t nsph = 0;
+    for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
+    // algorithmic bytes per body-step: 13 state reals read + 13
+    // written + constants (m, I[3], r | h[3])
+    w->bytes_per_body_step = (int64_t)w->esz * (26 + 4) + (int64_t)w->esz * ((nsph * 1 + (w->N - nsph) * 3) / w->N);
+
+    auto bail = [&](int rc) { free_world(w); return rc; };
+    if (hipSetDevice(w->device) != hipSuccess) return bail(fail(RB_ENODEV, "hipSetDevice(%d) failed", w->device));
+#define ALLOC(ptr, bytes)                                                                        \
+    do {                                                                                         \
+        if (hipMalloc((void **)&(ptr), (bytes)) != hipSuccess)                                   \
+            return bail(fail(RB_ENOMEM, "hipMalloc(%lld) failed", (long long)(bytes)));          \
+    } while (0)
+    ALLOC(w->gpos, (size_t)w->esz * 3 * w->Npad);
+    ALLOC(w->state, (size_t)w->esz * 10 * w->S);
+    ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
+    ALLOC(w->kind, sizeof(int32_t) * w->Npad);
+    const size_t entsz = w->dtype == RB_F64 ? sizeof(Entry<double>) : sizeof(Entry<float>);
+    for (int k = 0; k < 3; ++k) {
+        ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
+        ALLOC(w->ent[k], entsz * w->H * w->cap);
+    }
+    ALLOC(w->err, sizeof(int32_t));
+#undef ALLOC
+    if (hipHostMalloc((void **)&w->err_host, sizeof(int32_t), 0) != hipSuccess) return bail(fail(RB_ENOMEM, "hipHostMalloc failed"));
+    if (hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&w->cap_stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(RB_ENODEV, "hipStreamCreate failed"));
+    w->stream = w->own_stream;
+    if (hipMemset(w->gpos, 0, (size_t)w->esz * 3 * w->Npad) != hipSuccess ||
+        hipMemset(w->state, 0, (size_t)w->esz * 10 * w->S) != hipSuccess ||
+        hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
+        return bail(fail(RB_ENODEV, "hipMemset failed"));
+    int rc = w->dtype == RB_F64 ? upload_consts<double>(w, d) : upload_consts<float>(w, d);
+    if (rc) return bail(rc);
+    *out = w;
+    return RB_OK;
+}
+
+void rb_world_destroy(rb_world *w) { free_world(w); }
+
+int rb_set_stream(rb_world *w, void *s) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    w->stream = s ? (hipStream_t)s : w->own_stream;
+    return RB_OK;
+}
+
+int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
+    if (!w || !qpos || !qvel) return fail(RB_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(w->device));
+    int rc = w->dtype == RB_F64 ? upload_state<double>(w, qpos, qvel) : upload_state<float>(w, qpos, qvel);
+    w->primed = false;
+    return rc;
+}
+
+int rb_get_state(rb_world *w, double *qpos, double *qvel) {
+    if (!w || (!qpos && !qvel)) return fail(RB_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(w->device));
+    return w->dtype == RB_F64 ? download_state<double>(w, qpos, qvel) : download_state<float>(w, qpos, qvel);
+}
+
+int rb_set_xfrc(rb_world *w, const double *xf) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    HIPCHK(hipSetDevice(w->device));
+    if (!xf) {
+        if (w->xfrc) { HIPCHK(hipFree(w->xfrc)); w->xfrc = nullptr; }
+        for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+        w->graphs.clear();
+        return RB_OK;
+    }
+    if (!w->xfrc) HIPCHK(hipMalloc(&w->xfrc, (size_t)w->esz * 6 * w->S));
+    std::vector<double> h((size_t)6 * w->S, 0.0);
+    for (int64_t l = 0; l < w->n_local; ++l)
+        for (int d = 0; d < 6; ++d) h[(size_t)(d * w->S + l)] = xf[6 * (w->lo + l) + d];
+    if (w->dtype == RB_F64) {
+        HIPCHK(hipMemcpy(w->xfrc, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+    } else {
+        std::vector<float> f(h.begin(), h.end());
+        HIPCHK(hipMemcpy(w->xfrc, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice));
+    }
+    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+    w->graphs.clear();
+    return RB_OK;
+}
+
+int rb_step_async(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    return enqueue_steps(w, nsteps, dt, e, mu, thr);
+}
+
+int rb_sync(rb_world *w) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    HIPCHK(hipSetDevice(w->device));
+    return read_err(w);
+}
+
+int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    int rc = rb_step_async(w, nsteps, dt, e, mu, thr);
+    if (rc) return rc;
+    return read_err(w);
+}
+
+int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0)) return fail(RB_EINVAL, "invalid step parameters");
+    HIPCHK(hipSetDevice(w->device));
+    if (!w->primed) { int rc = prime(w); if (rc) return rc; }
+    if (w->timing) {
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+        HIPCHK(hipEventRecord(a, w->stream));
+        int rc = launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(b, w->stream));
+        w->tev.emplace_back(a, b);
+        if (w->tev.size() >= 4096) { int rc2 = collect_timing(w); if (rc2) return rc2; }
+        return RB_OK;
+    }
+    return launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+}
+
+int rb_shard_exchange_done(rb_world *w) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    HIPCHK(hipSetDevice(w->device));
+    const int nph = (w->phase + 1) % 3;
+    // insert every body not owned here into the next table (own ones went in
+    // from the step kernel)
+    hipError_t e = w->dtype == RB_F64
+                       ? launch_insert<double>(make_insert<double>(w, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream)
+                       : launch_insert<float>(make_insert<float>(w, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream);
+    HIPCHK(e);
+    w->phase = nph;
+    return RB_OK;
+}
+
+int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (dev_ptr) *dev_ptr = w->gpos;
+    if (shard_elems) *shard_elems = 3 * w->S;
+    if (elem_bytes) *elem_bytes = w->esz;
+    return RB_OK;
+}
+
+int rb_record_contacts(rb_world *w, int enable) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    HIPCHK(hipSetDevice(w->device));
+    if (enable && !w->rec_count) {
+        const size_t slots = (size_t)w->maxrec * (w->S > 0 ? w->S : 1);
+        HIPCHK(hipMalloc((void **)&w->rec_count, sizeof(int32_t) * w->S));
+        HIPCHK(hipMalloc((void **)&w->rec_partner, sizeof(int32_t) * slots));
+        HIPCHK(hipMalloc((void **)&w->rec_kind, sizeof(int32_t) * slots));
+        HIPCHK(hipMalloc(&w->rec_dist, (size_t)w->esz * slots));
+        HIPCHK(hipMemset(w->rec_count, 0, sizeof(int32_t) * w->S));
+    }
+    if (w->record != (enable != 0)) {
+        for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+        w->graphs.clear();
+    }
+    w->record = enable != 0;
+    return RB_OK;
+}
+
+int rb_get_contacts(rb_world *w, int32_t *counts, int32_t *partner, int32_t *kind, double *dist, int64_t cap,
+                    int64_t *total) {
+    if (!w || !counts) return fail(RB_EINVAL, "null argument");
+    if (!w->rec_count) return fail(RB_EINVAL, "contact recording was never enabled");
+    HIPCHK(hipSetDevice(w->device));
+    const size_t slots = (size_t)w->maxrec * w->S;
+    std::vector<int32_t> c((size_t)w->S), pa(slots), ki(slots);
+    std::vector<double> di(slots);
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipMemcpy(c.data(), w->rec_count, sizeof(int32_t) * w->S, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pa.data(), w->rec_partner, sizeof(int32_t) * slots, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ki.data(), w->rec_kind, sizeof(int32_t) * slots, hipMemcpyDeviceToHost));
+    if (w->dtype == RB_F64) {
+        HIPCHK(hipMemcpy(di.data(), w->rec_dist, sizeof(double) * slots, hipMemcpyDeviceToHost));
+    } else {
+        std::vector<float> f(slots);
+        HIPCHK(hipMemcpy(f.data(), w->rec_dist, sizeof(float) * slots, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < slots; ++k) di[k] = f[k];
+    }
+    int64_t t = 0;
+    for (int64_t l = 0; l < w->n_local; ++l) {
+        const int32_t n = c[(size_t)l] < w->maxrec ? c[(size_t)l] : w->maxrec;
+        counts[l] = c[(size_t)l];
+        for (int32_t k = 0; k < n; ++k, ++t) {
+            if (t < cap) {
+                const size_t o = (size_t)l * w->maxrec + k;
+                if (partner) partner[t] = pa[o];
+                if (kind) kind[t] = ki[o];
+                if (dist) dist[t] = di[o];
+            }
+        }
+    }
+    if (total) *total = t;
+    if (t > cap) return fail(RB_EOVERFLOW, "contact buffer too small: need %lld", (long long)t);
+    return RB_OK;
+}
+
+static int kat_common(int32_t device, int32_t dtype, int64_t n, const double *in, double *out, int nin, int nout,
+                      int which) {
+    if (n < 0 || (n && (!in || !out))) return fail(RB_EINVAL, "bad KAT arguments");
+    if (dtype != RB_F64 && dtype != RB_F32) return fail(RB_EINVAL, "bad dtype");
+    if (n == 0) return RB_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RB_ENODEV, "no HIP device available");
+    HIPCHK(hipSetDevice(device));
+    double *din = nullptr, *dout = nullptr;
+    HIPCHK(hipMalloc(&din, sizeof(double) * nin * n));
+    if (hipMalloc(&dout, sizeof(double) * nout * n) != hipSuccess) { (void)hipFree(din); return fail(RB_ENOMEM, "hipMalloc"); }
+    hipError_t e = hipMemcpy(din, in, sizeof(double) * nin * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        if (which == 1) e = dtype == RB_F64 ? launch_kat_inertia<double>(n, din, dout, nullptr) : launch_kat_inertia<float>(n, din, dout, nullptr);
+        else if (which == 2) e = dtype == RB_F64 ? launch_kat_apply<double>(n, din, dout, nullptr) : launch_kat_apply<float>(n, din, dout, nullptr);
+        else e = dtype == RB_F64 ? launch_kat_impulse<double>(n, din, dout, nullptr) : launch_kat_impulse<float>(n, din, dout, nullptr);
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * nout * n, hipMemcpyDeviceToHost);
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    HIPCHK(e);
+    return RB_OK;
+}
+
+int rb_kat_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    return kat_common(device, dtype, n, in, out, 24, 10, 0);
+}
+
+int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    return kat_common(device, dtype, n, in, out, 7, 18, 1);
+}
+
+int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    return kat_common(device, dtype, n, in, out, 26, 6, 2);
+}
+
+int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (n_owned) *n_owned = w->n_local;
+    if (bytes) *bytes = w->bytes_per_body_step;
+    return RB_OK;
+}
+
+int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    HIPCHK(hipSetDevice(w->device));
+    int rc = collect_timing(w);
+    if (rc) return rc;
+    if (avg_ms) *avg_ms = w->t_n ? w->t_sum_ms / (double)w->t_n : 0.0;
+    if (launches) *launches = w->t_n;
+    if (enable && !w->timing) { w->t_sum_ms = 0; w->t_n = 0; }
+    w->timing = enable != 0;
+    return RB_OK;
+}
+
+}  // extern "C"

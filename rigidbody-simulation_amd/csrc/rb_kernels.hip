@@ -1,0 +1,341 @@
+// rb_kernels.hip — the hot path on gfx950.
+//
+// One launch per simulation step (rb::step_kernel), one thread per owned
+// body, 64-thread workgroups (one wave):
+//   K1 contact generation  — plane-sphere / plane-box corners against the
+//      static planes, sphere-sphere against the broadphase snapshot of the
+//      step-start positions (spatial-hash buckets of the 27 neighbour cells);
+//      partners are kept in a per-lane sorted list in LDS (ascending body id
+//      = the canonical Gauss-Seidel order, SURVEY §7 hard part 1);
+//   K2 impulse solve       — per contact, in list order:
+//      compute_collision_impulse_friction (collision.py:7-48) then
+//      apply_impulse_friction (physics_utils.py:25-49);
+//   K3 integrate           — x += v dt, q += 0.5 (0,w)*q dt, normalise
+//      (collision.py:90-95), write SoA state in place;
+//   and the next step's broadphase: the body inserts its new position into
+//   the next table (atomic bucket slot) while the table two steps ahead is
+//   cleared by the whole grid.  Three tables rotate, so a step reads only a
+//   snapshot no thread of the same launch writes: Jacobi across bodies
+//   exactly as multi_sphere_bounce.py:43-46 (one mj_forward per step).
+#include "rb_device.hpp"
+#include "rb_internal.hpp"
+
+namespace rb {
+
+template <typename T> __device__ __forceinline__ uint32_t cell_hash(int32_t ix, int32_t iy, int32_t iz) {
+    return ((uint32_t)ix * 73856093u) ^ ((uint32_t)iy * 19349663u) ^ ((uint32_t)iz * 83492791u);
+}
+
+// cell coordinates; false (and ERR_DOMAIN) for non-finite / out-of-range
+template <typename T>
+__device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, int32_t &iy, int32_t &iz) {
+    const T fx = x * inv_cs, fy = y * inv_cs, fz = z * inv_cs;
+    const T lim = T(1 << 29);
+    if (!(absval(fx) < lim && absval(fy) < lim && absval(fz) < lim)) return false;
+    ix = (int32_t)__builtin_floor((double)fx);
+    iy = (int32_t)__builtin_floor((double)fy);
+    iz = (int32_t)__builtin_floor((double)fz);
+    return true;
+}
+
+template <typename T>
+__device__ __forceinline__ void insert_body(const Grid<T> &g, int32_t *cnt, Entry<T> *ent, int32_t *err,
+                                            T x, T y, T z, int32_t id) {
+    int32_t ix, iy, iz;
+    if (!cell_of(x, y, z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return; }
+    const uint32_t b = cell_hash<T>(ix, iy, iz) & g.hmask;
+    const int32_t slot = atomicAdd(cnt + b, 1);
+    if (slot >= g.cap) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    Entry<T> e;
+    e.x = x; e.y = y; e.z = z; e.id = id;
+    ent[(int64_t)b * g.cap + slot] = e;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= p.count) return;
+    const int64_t id = p.first + k;
+    if (id >= p.skip_lo && id < p.skip_hi) return;
+    const int64_t r = id / p.S, l = id - r * p.S;
+    const T *base = p.gpos + r * 3 * (int64_t)p.S;
+    insert_body(p.grid, p.cnt, p.ent, p.err, base[l], base[p.S + l], base[2 * (int64_t)p.S + l], (int32_t)id);
+}
+
+template <typename T>
+__device__ __forceinline__ void record(const StepParams<T> &p, int32_t l, int32_t &nrec, int32_t partner,
+                                       int32_t kind, T dist) {
+    if (!p.rec_count) return;
+    if (nrec < p.maxrec) {
+        const int64_t o = (int64_t)l * p.maxrec + nrec;
+        p.rec_partner[o] = partner;
+        p.rec_kind[o] = kind;
+        p.rec_dist[o] = dist;
+    }
+    ++nrec;
+}
+
+// one contact of body i through the reference's skip rules then K2
+template <typename T>
+__device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Contact<T> &con, V3<T> x, V3<T> n,
+                                              T m, const M3<T> &invI, V3<T> &v, V3<T> &w) {
+    if (!(con.dist < T(0))) return;                 // collision.py:74 (NaN fails too)
+    if (absval(con.dist) < p.thr) return;           // collision.py:79-80
+    const V3<T> r = {con.pos.x - x.x, con.pos.y - x.y, con.pos.z - x.z};   // :75
+    T jn;
+    V3<T> jt;
+    if (impulse(m, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI, r, n, jn, jt);
+}
+
+template <typename T, int MAXP>
+__global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
+    __shared__ int32_t s_id[MAXP * STEP_BLOCK];
+    __shared__ int32_t s_ent[MAXP * STEP_BLOCK];
+    const int tid = threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
+
+    // the table of step t+2 was last read by step t-1: clear it for t+1's inserts
+    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
+    if (gt >= p.n_local) return;
+    const int32_t l = (int32_t)gt;
+    const int32_t i = p.lo + l;
+
+    // ---- load (coalesced SoA) --------------------------------------------
+    V3<T> x = {p.st.px[l], p.st.py[l], p.st.pz[l]};
+    const Q4<T> q = {p.st.qw[l], p.st.qx[l], p.st.qy[l], p.st.qz[l]};
+    V3<T> v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
+    V3<T> w = {p.st.wx[l], p.st.wy[l], p.st.wz[l]};
+    const T m = p.cs.mass[i];
+    const V3<T> I = {p.cs.ix[i], p.cs.iy[i], p.cs.iz[i]};
+    const int32_t kind = p.cs.kind[i];
+    const V3<T> sz = {p.cs.sx[i], p.cs.sy[i], p.cs.sz[i]};
+
+    // ---- a3 + a4: world inertia, gravity / applied force -----------------
+    const M3<T> invI = np_inv3(inertia_world(I, q));                  // collision.py:62, :70
+    {
+        V3<T> F = {m * p.g[0], m * p.g[1], m * p.g[2]};                // :66
+        if (p.xfrc) {
+            F = {p.xfrc[l] + F.x, p.xfrc[p.S + l] + F.y, p.xfrc[2 * p.S + l] + F.z};
+        }
+        v = {v.x + (F.x / m) * p.dt, v.y + (F.y / m) * p.dt, v.z + (F.z / m) * p.dt};   // :69
+        if (p.xfrc) {
+            const V3<T> tdt = {p.xfrc[3 * p.S + l] * p.dt, p.xfrc[4 * p.S + l] * p.dt, p.xfrc[5 * p.S + l] * p.dt};
+            const V3<T> dw = np_matvec(invI, tdt);
+            w = {w.x + dw.x, w.y + dw.y, w.z + dw.z};
+        }
+    }
+
+    int32_t nrec = 0;
+    // ---- K1+K2: plane contacts, plane order --------------------------------
+    if (kind == 0) {
+        for (int pl = 0; pl < p.n_planes; ++pl) {
+            const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
+            const V3<T> pp = {p.pp[pl][0], p.pp[pl][1], p.pp[pl][2]};
+            Contact<T> con;
+            if (!plane_sphere(pn, pp, x, sz.x, con)) continue;
+            record(p, l, nrec, -1 - pl, 0, con.dist);
+            solve_contact(p, con, x, con.frame, m, invI, v, w);
+        }
+    } else {
+        const M3<T> M = mj_body_mat(q);
+        for (int pl = 0; pl < p.n_planes; ++pl) {
+            const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
+            const V3<T> dif = {x.x - p.pp[pl][0], x.y - p.pp[pl][1], x.z - p.pp[pl][2]};
+            const T dist = mj_dot(dif, pn);
+            int cnt = 0;
+            for (int c = 0; c < 8 && cnt < 4; ++c) {
+                Contact<T> con;
+                if (!plane_box_corner(pn, x, dist, M, sz, c, con)) continue;
+                ++cnt;
+                record(p, l, nrec, -1 - pl, 1 + c, con.dist);
+                solve_contact(p, con, x, con.frame, m, invI, v, w);
+            }
+        }
+    }
+
+    // ---- K1: broadphase over the 27 neighbour cells of the snapshot --------
+    int32_t np_ = 0;
+    bool overflow = false;
+    {
+        int32_t cx, cy, cz;
+        if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
+            atomicOr(p.err, ERR_DOMAIN);
+        } else {
+            const T bi = p.cs.bound[i];
+            for (int dz = -1; dz <= 1; ++dz)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const uint32_t b = cell_hash<T>(cx + dx, cy + dy, cz + dz) & p.grid.hmask;
+                        int32_t nb = p.cnt_cur[b];
+                        nb = nb < p.grid.cap ? nb : p.grid.cap;
+                        const int64_t base = (int64_t)b * p.grid.cap;
+                        for (int s = 0; s < nb; ++s) {
+                            const Entry<T> e = p.ent_cur[base + s];
+                            const int32_t j = e.id;
+                            if (j == i) continue;
+                            const V3<T> cj = {e.x, e.y, e.z};
+                            if (kind != 0 || p.cs.kind[j] != 0) {
+                                // box-involved pair: not restated
+                                const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
+                                if (sqroot(mj_dot(dd, dd)) <= bi + p.cs.bound[j]) atomicOr(p.err, ERR_UNSUPPORTED);
+                                continue;
+                            }
+                            if (!sphere_sphere_hit(x, sz.x, cj, p.cs.sx[j])) continue;
+                            // insert into the ascending-id list (dedupe: a bucket can
+                            // be reached from two neighbour cells after hashing)
+                            int pos = np_;
+                            bool dup = false;
+                            while (pos > 0) {
+                                const int32_t prev = s_id[(pos - 1) * STEP_BLOCK + tid];
+                                if (prev == j) { dup = true; break; }
+                                if (prev < j) break;
+                                --pos;
+                            }
+                            if (dup) continue;
+                            if (np_ >= MAXP) { overflow = true; continue; }
+                            for (int t = np_; t > pos; --t) {
+                                s_id[t * STEP_BLOCK + tid] = s_id[(t - 1) * STEP_BLOCK + tid];
+                                s_ent[t * STEP_BLOCK + tid] = s_ent[(t - 1) * STEP_BLOCK + tid];
+                            }
+                            s_id[pos * STEP_BLOCK + tid] = j;
+                            s_ent[pos * STEP_BLOCK + tid] = (int32_t)(base + s);
+                            ++np_;
+                        }
+                    }
+        }
+    }
+    if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
+
+    // ---- K2: sphere partners in ascending id order -------------------------
+    for (int s = 0; s < np_; ++s) {
+        const int32_t j = s_id[s * STEP_BLOCK + tid];
+        const Entry<T> e = p.ent_cur[s_ent[s * STEP_BLOCK + tid]];
+        const V3<T> cj = {e.x, e.y, e.z};
+        const T rj = p.cs.sx[j];
+        Contact<T> con;
+        V3<T> n;
+        if (i < j) {                        // this body is geom1
+            sphere_sphere(x, sz.x, cj, rj, con);
+            n = p.oriented ? V3<T>{-con.frame.x, -con.frame.y, -con.frame.z} : con.frame;
+        } else {
+            sphere_sphere(cj, rj, x, sz.x, con);
+            n = con.frame;
+        }
+        record(p, l, nrec, j, 16, con.dist);
+        solve_contact(p, con, x, n, m, invI, v, w);
+    }
+    if (p.rec_count) p.rec_count[l] = nrec;
+
+    // ---- K3: integrate (collision.py:90-100) -------------------------------
+    x = {x.x + v.x * p.dt, x.y + v.y * p.dt, x.z + v.z * p.dt};
+    const Q4<T> res = mj_mulquat(Q4<T>{T(0), w.x, w.y, w.z}, q);
+    Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
+                q.y + (T(0.5) * res.y) * p.dt, q.z + (T(0.5) * res.z) * p.dt};
+    const T nq = sqroot(fmadd(qn.z, qn.z, fmadd(qn.y, qn.y, fmadd(qn.x, qn.x, qn.w * qn.w))));
+    qn = {qn.w / nq, qn.x / nq, qn.y / nq, qn.z / nq};
+
+    p.st.px[l] = x.x; p.st.py[l] = x.y; p.st.pz[l] = x.z;
+    p.st.qw[l] = qn.w; p.st.qx[l] = qn.x; p.st.qy[l] = qn.y; p.st.qz[l] = qn.z;
+    p.st.vx[l] = v.x; p.st.vy[l] = v.y; p.st.vz[l] = v.z;
+    p.st.wx[l] = w.x; p.st.wy[l] = w.y; p.st.wz[l] = w.z;
+
+    // ---- next step's broadphase snapshot ----------------------------------
+    if (p.cnt_next) insert_body(p.grid, p.cnt_next, p.ent_next, p.err, x.x, x.y, x.z, i);
+}
+
+// ---- known-answer kernels ----------------------------------------------
+template <typename T>
+__global__ void kat_impulse_kernel(int64_t n, const double *in, double *out) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const double *a = in + 24 * c;
+    const T m = (T)a[0], e = (T)a[1], mu = (T)a[2];
+    V3<T> v = {(T)a[3], (T)a[4], (T)a[5]}, w = {(T)a[6], (T)a[7], (T)a[8]};
+    const V3<T> r = {(T)a[9], (T)a[10], (T)a[11]}, nn = {(T)a[12], (T)a[13], (T)a[14]};
+    M3<T> Iw;
+    for (int k = 0; k < 9; ++k) Iw.a[k] = (T)a[15 + k];
+    const M3<T> invI = np_inv3(Iw);
+    T jn;
+    V3<T> jt;
+    impulse(m, v, w, r, nn, e, mu, jn, jt);
+    apply(v, w, m, invI, r, nn, jn, jt);      // the reference always applies
+    double *o = out + 10 * c;
+    o[0] = jn; o[1] = jt.x; o[2] = jt.y; o[3] = jt.z;
+    o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = w.x; o[8] = w.y; o[9] = w.z;
+}
+
+template <typename T>
+__global__ void kat_inertia_kernel(int64_t n, const double *in, double *out) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const double *a = in + 7 * c;
+    const M3<T> Iw = inertia_world(V3<T>{(T)a[0], (T)a[1], (T)a[2]}, Q4<T>{(T)a[3], (T)a[4], (T)a[5], (T)a[6]});
+    const M3<T> Ii = np_inv3(Iw);
+    for (int k = 0; k < 9; ++k) { out[18 * c + k] = Iw.a[k]; out[18 * c + 9 + k] = Ii.a[k]; }
+}
+
+template <typename T>
+__global__ void kat_apply_kernel(int64_t n, const double *in, double *out) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const double *a = in + 26 * c;
+    const T m = (T)a[0];
+    V3<T> v = {(T)a[1], (T)a[2], (T)a[3]}, w = {(T)a[4], (T)a[5], (T)a[6]};
+    const V3<T> r = {(T)a[7], (T)a[8], (T)a[9]}, nn = {(T)a[10], (T)a[11], (T)a[12]};
+    const T jn = (T)a[13];
+    const V3<T> jt = {(T)a[14], (T)a[15], (T)a[16]};
+    M3<T> Iw;
+    for (int k = 0; k < 9; ++k) Iw.a[k] = (T)a[17 + k];
+    apply(v, w, m, np_inv3(Iw), r, nn, jn, jt);
+    double *o = out + 6 * c;
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = w.x; o[4] = w.y; o[5] = w.z;
+}
+
+// ---- launchers ----------------------------------------------------------
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, hipStream_t s) {
+    const int64_t work = p.n_local > p.grid.H ? p.n_local : p.grid.H;
+    int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
+    if (blocks < 1) blocks = 1;
+    (void)work;
+    if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    else hipLaunchKernelGGL((step_kernel<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
+template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s) {
+    if (p.count <= 0) return hipSuccess;
+    const int64_t blocks = (p.count + 255) / 256;
+    hipLaunchKernelGGL((insert_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((kat_impulse_kernel<T>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, in, out);
+    return hipGetLastError();
+}
+
+template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((kat_inertia_kernel<T>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, in, out);
+    return hipGetLastError();
+}
+
+template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((kat_apply_kernel<T>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, in, out);
+    return hipGetLastError();
+}
+
+template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_step<double>(const StepParams<double> &, int, hipStream_t);
+template hipError_t launch_step<float>(const StepParams<float> &, int, hipStream_t);
+template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
+template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
+template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_impulse<float>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_inertia<double>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_inertia<float>(int64_t, const double *, double *, hipStream_t);
+
+}  // namespace rb

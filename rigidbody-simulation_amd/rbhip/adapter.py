@@ -1,0 +1,167 @@
+"""Model/data adapter for the reference's step-function signatures.
+
+The reference step functions take MuJoCo's (model, data) and mutate
+data.qpos / data.qvel in place (collision.py:97-100,
+time_integeration.py:67-70, multi_sphere_bounce.py:85-88).  Here `model`
+is either
+
+  * a SceneModel (duck-typed MjModel built from an rbhip Scene or from the
+    MJCF loader, rbhip.mjcf) — the MuJoCo-free path, or
+  * a real mujoco.MjModel, when MuJoCo is installed for visualisation only
+    (read: body masses/inertias, free joints, plane/sphere/box geoms).
+
+The world (device state) is cached per model; every call uploads data's
+state, steps on the GPU and writes the result back into data, as the
+reference does per frame.
+"""
+from __future__ import annotations
+
+import warnings
+import weakref
+from typing import Optional
+
+import numpy as np
+
+from .scenes import BOX, GRAVITY, SPHERE, Scene
+from .world import World
+
+
+class _Opt:
+    def __init__(self, timestep: float, gravity):
+        self.timestep = float(timestep)
+        self.gravity = np.array(gravity, dtype=np.float64)
+
+
+class SceneModel:
+    """Duck-typed MjModel: body 0 = world, body 1 = the static plane body,
+    bodies 2.. = the free bodies (the order of models/sphere.xml, cube.xml)."""
+
+    FIRST = 2
+
+    def __init__(self, scene: Scene, names: Optional[list] = None):
+        self.rb_scene = scene
+        n = scene.n
+        self.nbody = n + self.FIRST
+        self.body_mass = np.zeros(self.nbody)
+        self.body_inertia = np.zeros((self.nbody, 3))
+        self.body_mass[self.FIRST:] = scene.mass
+        self.body_inertia[self.FIRST:] = scene.inertia
+        self.opt = _Opt(scene.dt, scene.gravity)
+        names = names or scene.names or [f"body{k}" for k in range(n)]
+        self.names = ["world", "plane_body"] + list(names)
+        self.nq, self.nv = 7 * n, 6 * n
+
+    def name2id(self, name: str) -> int:
+        try:
+            return self.names.index(name)
+        except ValueError:
+            return -1
+
+
+class SceneData:
+    """Duck-typed MjData: qpos [7N], qvel [6N], xfrc_applied [nbody, 6], time."""
+
+    def __init__(self, model: SceneModel):
+        sc = model.rb_scene
+        self.qpos = sc.qpos0.reshape(-1).copy()
+        self.qvel = sc.qvel0.reshape(-1).copy()
+        self.xfrc_applied = np.zeros((model.nbody, 6))
+        self.time = 0.0
+        self.ncon = 0
+
+
+def scene_from_mujoco(model) -> Scene:
+    """Scene from a compiled mujoco.MjModel (free bodies with one sphere or
+    box geom each; planes on static bodies).  Parity of this path is
+    unpinned: MuJoCo is not installed in the build container."""
+    import mujoco  # noqa: F401
+    d = mujoco.MjData(model)
+    mujoco.mj_forward(model, d)
+    free = [b for b in range(model.nbody) if model.body_jntnum[b] == 1 and
+            model.jnt_type[model.body_jntadr[b]] == mujoco.mjtJoint.mjJNT_FREE]
+    kind, size = [], []
+    planes = []
+    for g in range(model.ngeom):
+        t = model.geom_type[g]
+        if t == mujoco.mjtGeom.mjGEOM_PLANE:
+            mat = d.geom_xmat[g].reshape(3, 3)
+            planes.append(np.concatenate([mat[:, 2], d.geom_xpos[g]]))
+    for b in free:
+        gs = [g for g in range(model.ngeom) if model.geom_bodyid[g] == b]
+        if len(gs) != 1 or model.geom_type[gs[0]] not in (mujoco.mjtGeom.mjGEOM_SPHERE, mujoco.mjtGeom.mjGEOM_BOX):
+            raise NotImplementedError("each free body must carry exactly one sphere or box geom")
+        g = gs[0]
+        kind.append(SPHERE if model.geom_type[g] == mujoco.mjtGeom.mjGEOM_SPHERE else BOX)
+        size.append(model.geom_size[g].copy())
+    qpos = np.stack([d.qpos[model.jnt_qposadr[model.body_jntadr[b]]:][:7] for b in free])
+    qvel = np.stack([d.qvel[model.jnt_dofadr[model.body_jntadr[b]]:][:6] for b in free])
+    return Scene("mujoco", np.array(kind, np.int32), model.body_mass[free].copy(),
+                 model.body_inertia[free].copy(), np.array(size), np.array(planes).reshape(-1, 6),
+                 qpos, qvel, dt=float(model.opt.timestep), restitution=1.0, friction=0.5,
+                 gravity=np.array(model.opt.gravity, dtype=np.float64))
+
+
+_worlds: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_worlds_by_id: dict = {}
+
+
+def _scene_of(model) -> Scene:
+    sc = getattr(model, "rb_scene", None)
+    return sc if sc is not None else scene_from_mujoco(model)
+
+
+def world_for(model, normal_convention: str = "oriented") -> World:
+    try:
+        w = _worlds.get(model)
+    except TypeError:
+        w = _worlds_by_id.get(id(model))
+    if w is None:
+        w = World(_scene_of(model), normal_convention=normal_convention)
+        try:
+            _worlds[model] = w
+        except TypeError:
+            _worlds_by_id[id(model)] = w
+    return w
+
+
+def body_index(model, obj: str) -> int:
+    """mj_name2id(model, mjOBJ_BODY, obj) -> free-body index.  The reference
+    indexes model arrays with the raw id, so an unknown name (-1) selects the
+    LAST body (single_sphere_bounce.py:67 passes "sphere" for the
+    body "ball" and works by accident); reproduced, with a warning."""
+    nbody = getattr(model, "nbody", None)
+    bid = model.name2id(obj) if hasattr(model, "name2id") else -1
+    if bid < 0:
+        warnings.warn(f"body {obj!r} not found: using the last body, as mj_name2id's -1 does "
+                      f"in the reference (SURVEY D4)", stacklevel=3)
+        bid = nbody - 1
+    k = bid - SceneModel.FIRST
+    if k < 0:
+        raise ValueError(f"body {obj!r} is not a free body")
+    return k
+
+
+def step_model(model, data, nsteps: int, dt: float, restitution: float, friction: float,
+               threshold: float, normal_convention: str = "oriented") -> None:
+    """Upload data's state, run nsteps reference steps on the GPU, write back."""
+    w = world_for(model, normal_convention)
+    w.set_state(np.asarray(data.qpos).reshape(-1, 7), np.asarray(data.qvel).reshape(-1, 6))
+    xf = np.asarray(getattr(data, "xfrc_applied", np.zeros((1, 6))))
+    first = getattr(model, "FIRST", SceneModel.FIRST)
+    xf_free = xf[first:first + w.scene.n] if xf.shape[0] >= first + w.scene.n else None
+    w.set_xfrc(xf_free if xf_free is not None and np.any(xf_free) else None)
+    w.step(nsteps, dt=dt, restitution=restitution, friction=friction, threshold=threshold)
+    q, v = w.get_state()
+    data.qpos[:] = q.reshape(-1)
+    data.qvel[:] = v.reshape(-1)
+
+
+def load_scene_model(scene: Scene):
+    """(SceneModel, SceneData) for a Scene — what MjModel.from_xml_path +
+    MjData give the reference scripts."""
+    m = SceneModel(scene)
+    return m, SceneData(m)
+
+
+__all__ = ["SceneModel", "SceneData", "world_for", "step_model", "body_index", "load_scene_model",
+           "scene_from_mujoco", "GRAVITY"]

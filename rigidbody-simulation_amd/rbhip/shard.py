@@ -1,0 +1,108 @@
+"""Body-range sharding of one scene over the GPUs of a node.
+
+Rank r owns bodies [r*S, r*S + S), S = ceil(N / P).  Each step is Jacobi
+across bodies (multi_sphere_bounce.py:43-46: one contact pass, then every
+body updated from step-start data), and the reference treats a contact
+partner as static (collision.py:27), so a rank needs only the step-start
+POSITIONS of other ranks' bodies.  Per step:
+
+    rb_shard_step           owned bodies: contacts + impulses + integrate;
+                            new positions land in this rank's slice of the
+                            replicated [P][3][S] position buffer
+    all_gather_into_tensor  RCCL over xGMI (backend "nccl"), in place on the
+                            library's buffer, on the library's stream
+    rb_shard_exchange_done  publish the other ranks' positions to the
+                            broadphase of the next step
+
+Contacts are generated from identical global positions with global body
+ids in a canonical order, so fp64 results are bit-identical for any P.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+from .scenes import Scene
+from .world import World
+
+
+class _DeviceBuffer:
+    """__cuda_array_interface__ view of library-owned device memory, so torch
+    can wrap it without a copy (torch.as_tensor consumes the interface)."""
+
+    def __init__(self, ptr: int, n: int, esz: int):
+        self.__cuda_array_interface__ = {
+            "shape": (n,), "typestr": "<f8" if esz == 8 else "<f4", "data": (ptr, False),
+            "version": 2, "strides": None, "stream": None}
+
+
+def wrap_gpos(world: World, torch):
+    ptr, shard_elems, esz = world.gpos_buffer()
+    total = shard_elems * world.world_size
+    t = torch.as_tensor(_DeviceBuffer(ptr, total, esz), device=f"cuda:{torch.cuda.current_device()}")
+    return t, shard_elems
+
+
+class ShardedWorld:
+    """One rank's shard of a scene; `step` runs the exchange each step.
+
+    transport: "nccl" (RCCL all-gather on device memory; the default when the
+    process group backend is nccl) or "host" (stage through host memory, for
+    gloo process groups, e.g. several ranks sharing one GPU in tests)."""
+
+    def __init__(self, scene: Scene, dtype: str = "f64", device: Optional[int] = None,
+                 group=None, transport: Optional[str] = None, **world_kw):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.P = dist.get_world_size(group)
+            backend = dist.get_backend(group)
+        else:
+            self.rank, self.P, backend = 0, 1, None
+        if device is None:
+            device = torch.cuda.current_device()
+        torch.cuda.set_device(device)
+        self.transport = transport or ("nccl" if backend == "nccl" else "host")
+        self.world = World(scene, device=device, dtype=dtype, rank=self.rank, world_size=self.P,
+                           **world_kw)
+        self.stream = torch.cuda.current_stream(device)
+        self.world.set_stream(self.stream.cuda_stream)
+        self.gpos, self.shard_elems = wrap_gpos(self.world, torch)
+        self.mine = self.gpos[self.rank * self.shard_elems:(self.rank + 1) * self.shard_elems]
+
+    def _exchange(self):
+        if self.transport == "nccl":
+            # in place: the input is this rank's chunk of the output buffer
+            self.dist.all_gather_into_tensor(self.gpos, self.mine, group=self.group)
+        else:
+            cpu = self.mine.to("cpu")
+            out = self.torch.empty(self.P * self.shard_elems, dtype=cpu.dtype)
+            self.dist.all_gather_into_tensor(out, cpu, group=self.group)
+            self.gpos.copy_(out.to(self.gpos.device))
+
+    def step(self, nsteps: int = 1, **params):
+        if self.P == 1:
+            self.world.step_async(nsteps, **params)
+            return
+        for _ in range(nsteps):
+            self.world.shard_step(**params)
+            self._exchange()
+            self.world.shard_exchange_done()
+
+    def sync(self):
+        self.world.sync()
+
+    def gather_state(self):
+        """Full (qpos, qvel) on every rank (host all-gather of owned rows)."""
+        q, v = self.world.get_state()
+        if self.P == 1:
+            return q, v
+        t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
+        if self.transport == "nccl":
+            t = t.to(self.gpos.device)
+        self.dist.all_reduce(t, group=self.group)      # rows are disjoint: sum == union
+        a = t.cpu().numpy()
+        return a[:, :7].copy(), a[:, 7:].copy()

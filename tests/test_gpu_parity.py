@@ -1,0 +1,246 @@
+"""Parity of the HIP path (librbhip.so through the C-ABI) against the goldens
+produced by the reference's own functions and against the oracle.
+
+Bar: fp64 bit-exact (contacts AND state) — the kernels keep the reference's
+operation order; fp32 bit-exact against the fp32 restatement; fp32 vs fp64
+within the SURVEY §8d sweep tolerance."""
+import ctypes as C
+import time
+
+import numpy as np
+import pytest
+
+from conftest import NBODY_GOLDENS, golden_scene, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rb():
+    import rbhip
+    rbhip.load()
+    return rbhip
+
+
+# ---------------------------------------------------------------- KATs
+def test_kat_impulse_device_bit_exact(rb):
+    g = load_golden("kat_impulse")
+    out = rb.kat_impulse(g["inp"])
+    bad = np.nonzero((out != g["out"]).any(1))[0]
+    assert bad.size == 0, f"{bad.size} KAT rows differ, first {bad[:5]}: {out[bad[:1]]} vs {g['out'][bad[:1]]}"
+
+
+def test_kat_inertia_device_bit_exact(rb):
+    g = load_golden("kat_inertia")
+    out = rb.kat_inertia(g["inp"])
+    assert np.array_equal(out, g["out"])
+
+
+def test_kat_f32_matches_f32_restatement(rb, oracle):
+    g = load_golden("kat_impulse")
+    assert np.array_equal(rb.kat_impulse(g["inp"], dtype="f32"), oracle.kat_impulse(g["inp"], dtype="f32"))
+    g = load_golden("kat_inertia")
+    assert np.array_equal(rb.kat_inertia(g["inp"], dtype="f32"), oracle.kat_inertia(g["inp"], dtype="f32"))
+
+
+# ---------------------------------------------------------------- goldens
+@pytest.mark.parametrize("name", ["traj_single_sphere", "traj_single_cube"])
+def test_single_body_trajectory_vs_reference(rb, name):
+    g = load_golden(name)
+    with rb.World(golden_scene(g)) as w:
+        for t in range(0, 2000, 100):           # graph-replayed 100-step chunks
+            w.step(100)
+            q, v = w.get_state()
+            assert np.array_equal(q[0], g["qpos"][t + 100]), f"{name}: qpos differs after step {t + 100}"
+            assert np.array_equal(v[0], g["qvel"][t + 100]), f"{name}: qvel differs after step {t + 100}"
+
+
+@pytest.mark.parametrize("name", NBODY_GOLDENS)
+def test_nbody_golden_contacts_and_state(rb, name):
+    g = load_golden(name)
+    with rb.World(golden_scene(g)) as w:
+        w.record_contacts(True)
+        snaps = list(g["snap_step"])
+        si = 1
+        for t in range(snaps[-1]):
+            w.step(1)
+            if t < len(g["c_counts"]):
+                cnt, par, kin, dis = w.contacts()
+                a, b = g["c_off"][t], g["c_off"][t + 1]
+                assert np.array_equal(cnt, g["c_counts"][t]), f"contact counts differ at step {t}"
+                assert np.array_equal(par, g["c_partner"][a:b]), f"partners differ at step {t}"
+                assert np.array_equal(kin, g["c_kind"][a:b]), f"kinds differ at step {t}"
+                assert np.array_equal(dis, g["c_dist"][a:b]), f"dists differ at step {t}"
+            if si < len(snaps) and t + 1 == snaps[si]:
+                q, v = w.get_state()
+                assert np.array_equal(q, g["qpos"][si]), f"qpos differs at step {t + 1}"
+                assert np.array_equal(v, g["qvel"][si]), f"qvel differs at step {t + 1}"
+                si += 1
+
+
+# ---------------------------------------------------------------- oracle at scale
+def _oracle_run(oracle, sc, steps, dtype="f64", record=False):
+    osc = oracle.OracleScene(sc)
+    return oracle.step(osc, sc.qpos0, sc.qvel0, steps, dtype=dtype, record=record)
+
+
+@pytest.mark.parametrize("cfg,steps", [("c2", 300), ("c4", 40), ("c5", 120)])
+def test_config_trajectory_bit_exact_vs_oracle(rb, oracle, cfg, steps):
+    from rbhip import scenes
+    sc = scenes.make(cfg)
+    q0, v0, (cnt, par, kin, dis) = _oracle_run(oracle, sc, steps, record=True)
+    with rb.World(sc) as w:
+        w.step(steps - 1)                 # graph path
+        w.record_contacts(True)
+        w.step(1)                         # single-launch path, recorded
+        q, v = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert np.array_equal(gd, dis)
+    assert np.array_equal(q, q0) and np.array_equal(v, v0)
+    assert (kin == 16).any() or cfg == "c5"          # sphere-sphere contacts present
+
+
+def test_c3_one_step_parity_from_evolved_state(rb, oracle):
+    """65,536 spheres: 30 oracle steps, then one GPU step from that state vs
+    one oracle step (contacts and state bit-exact)."""
+    from rbhip import scenes
+    sc = scenes.make("c3")
+    osc = oracle.OracleScene(sc)
+    q, v = oracle.step(osc, sc.qpos0, sc.qvel0, 30)
+    q1, v1, (cnt, par, kin, dis) = oracle.step(osc, q, v, 1, record=True)
+    with rb.World(sc.with_(qpos0=q, qvel0=v)) as w:
+        w.record_contacts(True)
+        w.step(1)
+        gq, gv = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert np.array_equal(gq, q1) and np.array_equal(gv, v1)
+
+
+def test_f32_bit_exact_vs_f32_restatement(rb, oracle):
+    from rbhip import scenes
+    sc = scenes.make("c2")
+    q0, v0 = _oracle_run(oracle, sc, 150, dtype="f32")
+    with rb.World(sc, dtype="f32") as w:
+        w.step(150)
+        q, v = w.get_state()
+    assert np.array_equal(q, q0) and np.array_equal(v, v0)
+
+
+def test_f32_vs_f64_tolerance_sweep(rb):
+    """C3 sweep: fp32 stays close to fp64 over a short horizon."""
+    from rbhip import scenes
+    sc = scenes.make("c3")
+    out = {}
+    for dt in ("f64", "f32"):
+        with rb.World(sc, dtype=dt) as w:
+            w.step(100)
+            out[dt] = w.get_state()[0]
+    d = np.abs(out["f32"][:, :3] - out["f64"][:, :3])
+    assert np.median(d) < 1e-4 and d.max() < 0.5
+
+
+def test_xfrc_applied_matches_oracle(rb, oracle):
+    from rbhip import scenes
+    sc = scenes.flat_spheres(16, 16, seed=5)
+    rng = np.random.default_rng(0)
+    xf = rng.normal(0, 0.5, (sc.n, 6))
+    osc = oracle.OracleScene(sc)
+    q0, v0 = oracle.step(osc, sc.qpos0, sc.qvel0, 80, xfrc=xf)
+    with rb.World(sc) as w:
+        w.set_xfrc(xf)
+        w.step(80)
+        q, v = w.get_state()
+    assert np.array_equal(q, q0) and np.array_equal(v, v0)
+
+
+# ---------------------------------------------------------------- determinism / sharding
+def test_graph_equals_single_launches_and_reruns(rb):
+    from rbhip import scenes
+    sc = scenes.make("c2")
+    res = []
+    for mode in ("graph", "single", "graph"):
+        with rb.World(sc) as w:
+            if mode == "graph":
+                w.step(200)
+            else:
+                for _ in range(200):
+                    w.step_async(1)
+                w.sync()
+            res.append(w.get_state())
+    for q, v in res[1:]:
+        assert np.array_equal(q, res[0][0]) and np.array_equal(v, res[0][1])
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_shard_invariance_in_process(rb, P):
+    """P body-range shards on one device, positions exchanged by device copies
+    between their replicated buffers: bit-identical to one world."""
+    import torch
+    from rbhip import scenes
+    from rbhip.shard import wrap_gpos
+    sc = scenes.flat_spheres(32, 25, seed=7)          # N = 800 (not a multiple of 3)
+    with rb.World(sc) as ref:
+        ref.step(120)
+        rq, rv = ref.get_state()
+    worlds = [rb.World(sc, rank=r, world_size=P) for r in range(P)]
+    bufs = [wrap_gpos(w, torch) for w in worlds]
+    S3 = bufs[0][1]
+    for _ in range(120):
+        for w in worlds:
+            w.shard_step()
+        for w in worlds:
+            w.sync()
+        for r, (buf, _) in enumerate(bufs):
+            for o, (obuf, _) in enumerate(bufs):
+                if o != r:
+                    buf[o * S3:(o + 1) * S3].copy_(obuf[o * S3:(o + 1) * S3])
+        torch.cuda.synchronize()
+        for w in worlds:
+            w.shard_exchange_done()
+    q = np.zeros((sc.n, 7))
+    v = np.zeros((sc.n, 6))
+    for w in worlds:
+        w.get_state(q, v)
+        w.close()
+    assert np.array_equal(q, rq) and np.array_equal(v, rv)
+
+
+# ---------------------------------------------------------------- loud failures
+def test_bucket_or_partner_overflow_is_an_error(rb):
+    from rbhip import scenes
+    sc = scenes.flat_spheres(6, 6, seed=0)
+    q = sc.qpos0.copy()
+    q[:, 0:3] = [0.0, 0.0, 1.0]                       # 36 spheres at one point
+    with rb.World(sc.with_(qpos0=q)) as w:
+        with pytest.raises(rb.RbError, match="EOVERFLOW"):
+            w.step(1)
+
+
+def test_nonfinite_position_is_an_error(rb):
+    from rbhip import scenes
+    sc = scenes.flat_spheres(4, 4, seed=0)
+    q = sc.qpos0.copy()
+    q[3, 2] = np.nan
+    with rb.World(sc.with_(qpos0=q)) as w:
+        with pytest.raises(rb.RbError, match="EDOM"):
+            w.step(1)
+
+
+def test_box_pair_is_unsupported(rb):
+    from rbhip import scenes
+    sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)
+    with rb.World(sc) as w:
+        with pytest.raises(rb.RbError, match="EUNSUPPORTED"):
+            w.step(1)
+
+
+def test_kernel_timing_reports_launches(rb):
+    from rbhip import scenes
+    with rb.World(scenes.make("c2")) as w:
+        w.kernel_timing(True)
+        w.step(20)
+        avg, n = w.kernel_timing(False)
+    assert n == 20 and 0 < avg < 50.0
+    assert C.sizeof(C.c_double) == 8 and time.time() > 0

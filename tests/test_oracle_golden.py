@@ -1,0 +1,108 @@
+"""The oracle (C restatement) against vectors produced by the reference's own
+functions (tests/golden/make_golden.py).  Bit-exact: the oracle restates the
+reference arithmetic in NumPy's operation order."""
+import numpy as np
+import pytest
+
+from conftest import NBODY_GOLDENS, golden_scene, load_golden
+
+
+def test_kat_impulse_bit_exact(oracle):
+    g = load_golden("kat_impulse")
+    out = oracle.kat_impulse(g["inp"])
+    assert np.array_equal(out, g["out"]), "a1+a2 KAT mismatch (collision.py:7-48, physics_utils.py:25-49)"
+
+
+def test_kat_impulse_covers_edge_cases():
+    g = load_golden("kat_impulse")
+    inp, out = g["inp"], g["out"]
+    # separating / exactly-zero normal velocity rows give jn == 0, jt == 0
+    assert ((out[:, 0] == 0) & (np.abs(out[:, 1:4]).sum(1) == 0)).sum() >= 2
+    # friction cut-off rows around |u_t| = 1e-6
+    ut = np.abs(inp[:, 3])
+    assert np.any(ut == 1e-6) and np.any(ut == np.nextafter(1e-6, 0)) and np.any(ut == np.nextafter(1e-6, 1))
+    assert np.any(inp[:, 1] == 0.0) and np.any(inp[:, 1] == 1.0) and np.any(inp[:, 2] == 0.0)
+
+
+def test_kat_inertia_bit_exact(oracle):
+    g = load_golden("kat_inertia")
+    out = oracle.kat_inertia(g["inp"])
+    assert np.array_equal(out, g["out"]), "compute_inertia_tensor_world / np.linalg.inv mismatch"
+
+
+@pytest.mark.parametrize("name", ["traj_single_sphere", "traj_single_cube"])
+def test_single_body_trajectory_bit_exact(oracle, name):
+    g = load_golden(name)
+    sc = golden_scene(g)
+    osc = oracle.OracleScene(sc)
+    q, v = g["qpos0"], g["qvel0"]
+    for t in range(0, 2000, 100):          # 100-step chunks; compare at chunk ends
+        q, v = oracle.step(osc, q, v, 100)
+        assert np.array_equal(q[0], g["qpos"][t + 100]), f"{name}: qpos differs after step {t + 100}"
+        assert np.array_equal(v[0], g["qvel"][t + 100]), f"{name}: qvel differs after step {t + 100}"
+
+
+def test_single_sphere_reproduces_reference_plot():
+    """data/plots/single_sphere/height_vs_time.png: local maxima of
+    z at (t, z) = (1.116, 1.478), (2.061, 1.109), (2.871, 0.845), ...
+    and x, y drifting to about (0.62, -0.62) by t = 5.2 s."""
+    g = load_golden("traj_single_sphere")
+    z = g["qpos"][:, 2]
+    t = np.arange(len(z)) * 0.009
+    peaks = [k for k in range(1, len(z) - 1) if z[k] > z[k - 1] and z[k] >= z[k + 1]]
+    got = [(round(t[k], 3), round(z[k], 3)) for k in peaks[:7]]
+    want = [(1.116, 1.478), (2.061, 1.109), (2.871, 0.845), (3.555, 0.666), (4.122, 0.541),
+            (4.617, 0.451), (5.049, 0.386)]
+    for (tg, zg), (tw, zw) in zip(got, want):
+        assert abs(tg - tw) <= 0.0095 and abs(zg - zw) <= 0.002, (got, want)
+    k = int(round(5.2 / 0.009))
+    assert abs(g["qpos"][k, 0] - 0.62) < 0.03 and abs(g["qpos"][k, 1] + 0.62) < 0.03
+
+
+@pytest.mark.parametrize("name", NBODY_GOLDENS)
+def test_nbody_trajectory_and_contacts_bit_exact(oracle, name):
+    g = load_golden(name)
+    sc = golden_scene(g)
+    osc = oracle.OracleScene(sc)
+    q, v = g["qpos0"], g["qvel0"]
+    snaps = list(g["snap_step"])
+    si = 1
+    for t in range(snaps[-1]):
+        q, v, (cnt, par, kin, dis) = oracle.step(osc, q, v, 1, record=True)
+        if t < len(g["c_counts"]):
+            a, b = g["c_off"][t], g["c_off"][t + 1]
+            assert np.array_equal(cnt, g["c_counts"][t]), f"contact counts differ at step {t}"
+            assert np.array_equal(par, g["c_partner"][a:b]), f"contact partners differ at step {t}"
+            assert np.array_equal(kin, g["c_kind"][a:b]), f"contact kinds differ at step {t}"
+            assert np.array_equal(dis, g["c_dist"][a:b]), f"contact dists differ at step {t}"
+        if si < len(snaps) and t + 1 == snaps[si]:
+            assert np.array_equal(q, g["qpos"][si]), f"qpos differs at step {t + 1}"
+            assert np.array_equal(v, g["qvel"][si]), f"qvel differs at step {t + 1}"
+            si += 1
+
+
+def test_goldens_exercise_contacts():
+    """The N-body goldens must actually contain plane and sphere-sphere
+    contacts (and box corners), or the bit-exact checks above are vacuous."""
+    kinds = {n: set(np.unique(load_golden(n)["c_kind"]).tolist()) for n in NBODY_GOLDENS}
+    assert 16 in kinds["traj_flat64"] and 0 in kinds["traj_flat64"]
+    assert 16 in kinds["traj_flat256"] and 16 in kinds["traj_flat64_raw"]
+    assert any(1 <= k <= 8 for k in kinds["traj_cubes16"])
+
+
+def test_oracle_f32_close_to_f64(oracle):
+    """The fp32 restatement (what the f32 kernel must reproduce bit for bit)
+    stays near the fp64 trajectory on a non-chaotic scene."""
+    g = load_golden("traj_single_sphere")
+    sc = golden_scene(g)
+    osc = oracle.OracleScene(sc)
+    q64, _ = oracle.step(osc, g["qpos0"], g["qvel0"], 300)
+    q32, _ = oracle.step(osc, g["qpos0"], g["qvel0"], 300, dtype="f32")
+    assert np.abs(q64 - q32).max() < 1e-3
+
+
+def test_oracle_rejects_box_pairs(oracle):
+    from rbhip import scenes
+    sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)    # cubes overlapping
+    with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
+        oracle.step(oracle.OracleScene(sc), sc.qpos0, sc.qvel0, 1)
