@@ -150,6 +150,8 @@ template <typename T> InsertParams<T> make_insert(rb_world *w, int ph, int64_t f
                                                   int64_t skip_lo, int64_t skip_hi) {
     InsertParams<T> ip{};
     ip.gpos = dp<T>(w->gpos, 0);
+    ip.bound = dp<T>(w->consts, 7 * w->Npad);
+    ip.kind = w->kind;
     ip.S = (int32_t)w->S;
     ip.first = first; ip.count = count; ip.skip_lo = skip_lo; ip.skip_hi = skip_hi;
     ip.grid.inv_cs = (T)w->inv_cs;
@@ -340,7 +342,8 @@ int upload_consts(rb_world *w, const rb_scene_desc *d) {
         }
         c[(size_t)(7 * w->Npad + b)] = (T)bound;
     }
-    const double cs = rmax > 0 ? 2.0 * rmax * 1.001 : 1.0;
+    // cell = 2 x the largest contact reach (2 x 2 rmax): the 2x2x2 query
+    const double cs = rmax > 0 ? 4.0 * rmax * 1.001 : 1.0;
     w->inv_cs = 1.0 / cs;
     HIPCHK(hipMemcpy(w->consts, c.data(), sizeof(T) * c.size(), hipMemcpyHostToDevice));
     std::vector<int32_t> k((size_t)w->Npad, 0);
@@ -413,7 +416,12 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxp = maxp;
     w->cap = d->bucket_capacity > 0 ? d->bucket_capacity : 16;
     w->maxrec = 4 * w->n_planes + w->maxp;
-    w->H = next_pow2(2 * w->N > 1024 ? 2 * w->N : 1024);
+    // buckets: >= 4 per body and >= 256 tiles of 256 (spatially coherent
+    // tiles are hashed; keep tile collisions rare)
+#ifndef RB_HMULT
+#define RB_HMULT 4
+#endif
+    w->H = next_pow2(RB_HMULT * w->N > 65536 ? RB_HMULT * w->N : 65536);
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
     // algorithmic bytes per body-step: 13 state reals read + 13

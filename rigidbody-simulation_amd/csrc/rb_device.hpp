@@ -181,15 +181,12 @@ template <typename T> __device__ M3<T> mj_body_mat(Q4<T> q) {
         const T inv = T(1) / nrm;
         q = {q.w * inv, q.x * inv, q.y * inv, q.z * inv};
     }
-    M3<T> M;
-    if (q.w == T(1) && q.x == T(0) && q.y == T(0) && q.z == T(0)) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) M.a[k] = (k % 4 == 0) ? T(1) : T(0);
-        return M;
-    }
+    // mju_quat2Mat's identity shortcut, as selects (no early return)
+    const bool ident = (q.w == T(1) && q.x == T(0) && q.y == T(0) && q.z == T(0));
     const T q00 = q.w * q.w, q01 = q.w * q.x, q02 = q.w * q.y, q03 = q.w * q.z;
     const T q11 = q.x * q.x, q12 = q.x * q.y, q13 = q.x * q.z;
     const T q22 = q.y * q.y, q23 = q.y * q.z, q33 = q.z * q.z;
+    M3<T> M;
     M.a[0] = q00 + q11 - q22 - q33;
     M.a[4] = q00 - q11 + q22 - q33;
     M.a[8] = q00 - q11 - q22 + q33;
@@ -199,6 +196,10 @@ template <typename T> __device__ M3<T> mj_body_mat(Q4<T> q) {
     M.a[5] = T(2) * (q23 - q01);
     M.a[6] = T(2) * (q13 - q02);
     M.a[7] = T(2) * (q23 + q01);
+    if (ident) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) M.a[k] = (k % 4 == 0) ? T(1) : T(0);
+    }
     return M;
 }
 

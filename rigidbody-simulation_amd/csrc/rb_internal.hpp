@@ -15,10 +15,12 @@ enum : int32_t {
     ERR_DOMAIN = 8,             // non-finite / out-of-range position
 };
 
-// Broadphase bucket entry: a snapshot of a body's step-start position.
+// Broadphase bucket entry: a snapshot of a body's step-start position plus
+// what a candidate test needs (bounding radius == sphere radius for spheres,
+// body kind), so the query reads nothing else by body id.
 template <typename T> struct Entry;
-template <> struct alignas(32) Entry<double> { double x, y, z; int32_t id; int32_t pad; };
-template <> struct alignas(16) Entry<float> { float x, y, z; int32_t id; };
+template <> struct alignas(16) Entry<double> { double x, y, z, r; int32_t id, kind; int32_t pad[2]; };
+template <> struct alignas(16) Entry<float> { float x, y, z, r; int32_t id, kind; int32_t pad[2]; };
 
 constexpr int MAX_PLANES = 8;
 
@@ -73,6 +75,8 @@ template <typename T> struct StepParams {
 
 template <typename T> struct InsertParams {
     const T *gpos;                     // [P][3][S]
+    const T *bound;                    // [Npad] bounding radius
+    const int32_t *kind;               // [Npad]
     int32_t S;
     int64_t first, count;              // global ids [first, first+count)
     int64_t skip_lo, skip_hi;          // global ids to skip (already inserted)

@@ -20,10 +20,56 @@
 #include "rb_device.hpp"
 #include "rb_internal.hpp"
 
+// diagnostic builds only (scripts/ablate.py): 1 = skip the sphere-sphere
+// broadphase, 2 = skip the world-inertia inverse (identity), 0 = product
+#ifndef RB_ABLATE
+#define RB_ABLATE 0
+#endif
+// diagnostic build only: per-wave s_memtime stamps at phase boundaries
+#ifndef RB_STAMPS
+#define RB_STAMPS 0
+#endif
+#if RB_STAMPS
+__device__ unsigned long long rb_stamp_buf[1 << 16][8];
+#define STAMP(k)                                                                                  \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if (tid == 0 && blockIdx.x < (1u << 16)) rb_stamp_buf[blockIdx.x][k] = t_;                \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+// candidates whose entry loads are issued together
+#ifndef RB_QBATCH
+#define RB_QBATCH 4
+#endif
+
 namespace rb {
 
-template <typename T> __device__ __forceinline__ uint32_t cell_hash(int32_t ix, int32_t iy, int32_t iz) {
-    return ((uint32_t)ix * 73856093u) ^ ((uint32_t)iy * 19349663u) ^ ((uint32_t)iz * 83492791u);
+// tile coordinate -> well-mixed 32-bit hash (murmur3 finaliser)
+__device__ __forceinline__ uint32_t tile_hash(int32_t ix, int32_t iy, int32_t iz) {
+    uint32_t h = (uint32_t)ix * 0x8da6b343u + (uint32_t)iy * 0xd8163841u + (uint32_t)iz * 0xcb1ab31fu;
+    h ^= h >> 16; h *= 0x85ebca6bu;
+    h ^= h >> 13; h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+// Spatially coherent bucket of a cell: 8x8x4-cell tiles are contiguous runs
+// of 256 buckets (x fastest), whole tiles are hashed.  Neighbouring cells —
+// and so the queries of neighbouring bodies — share cache lines.
+__device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, uint32_t hmask) {
+    const uint32_t t = tile_hash(ix >> 3, iy >> 3, iz >> 2);
+    return ((t << 8) | ((uint32_t)(iz & 3) << 6) | ((uint32_t)(iy & 7) << 3) | (uint32_t)(ix & 7)) & hmask;
+}
+
+// Entries are slot-major within a tile: [tile][slot][256 cells], so the
+// first entries of adjacent cells are adjacent in memory.
+__device__ __forceinline__ int64_t entry_index(uint32_t b, int32_t slot, int32_t cap) {
+    return ((int64_t)(b >> 8) * cap + slot) * 256 + (b & 255u);
 }
 
 // cell coordinates; false (and ERR_DOMAIN) for non-finite / out-of-range
@@ -40,15 +86,15 @@ __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, in
 
 template <typename T>
 __device__ __forceinline__ void insert_body(const Grid<T> &g, int32_t *cnt, Entry<T> *ent, int32_t *err,
-                                            T x, T y, T z, int32_t id) {
+                                            T x, T y, T z, T r, int32_t id, int32_t kind) {
     int32_t ix, iy, iz;
     if (!cell_of(x, y, z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return; }
-    const uint32_t b = cell_hash<T>(ix, iy, iz) & g.hmask;
+    const uint32_t b = bucket_of(ix, iy, iz, g.hmask);
     const int32_t slot = atomicAdd(cnt + b, 1);
     if (slot >= g.cap) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
     Entry<T> e;
-    e.x = x; e.y = y; e.z = z; e.id = id;
-    ent[(int64_t)b * g.cap + slot] = e;
+    e.x = x; e.y = y; e.z = z; e.r = r; e.id = id; e.kind = kind; e.pad[0] = 0; e.pad[1] = 0;
+    ent[entry_index(b, slot, g.cap)] = e;
 }
 
 template <typename T>
@@ -59,7 +105,8 @@ __global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
     if (id >= p.skip_lo && id < p.skip_hi) return;
     const int64_t r = id / p.S, l = id - r * p.S;
     const T *base = p.gpos + r * 3 * (int64_t)p.S;
-    insert_body(p.grid, p.cnt, p.ent, p.err, base[l], base[p.S + l], base[2 * (int64_t)p.S + l], (int32_t)id);
+    insert_body(p.grid, p.cnt, p.ent, p.err, base[l], base[p.S + l], base[2 * (int64_t)p.S + l], p.bound[id],
+                (int32_t)id, p.kind[id]);
 }
 
 template <typename T>
@@ -75,16 +122,126 @@ __device__ __forceinline__ void record(const StepParams<T> &p, int32_t l, int32_
     ++nrec;
 }
 
+// Lazily evaluated inv(inertia_world): the reference computes it every step
+// (collision.py:62) but it only reaches the state through a torque or an
+// applied impulse; computing it on first use is value-identical and keeps
+// it out of the broadphase's register live range.
+template <typename T> struct LazyInvI {
+    V3<T> I;
+    Q4<T> q;
+    bool have = false;
+    M3<T> m;
+    __device__ __forceinline__ const M3<T> &get() {
+        if (!have) {
+#if RB_ABLATE == 2
+            for (int k = 0; k < 9; ++k) m.a[k] = (k % 4 == 0) ? T(1) / I.x : T(0);
+#else
+            m = np_inv3(inertia_world(I, q));
+#endif
+            have = true;
+        }
+        return m;
+    }
+};
+
 // one contact of body i through the reference's skip rules then K2
 template <typename T>
 __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Contact<T> &con, V3<T> x, V3<T> n,
-                                              T m, const M3<T> &invI, V3<T> &v, V3<T> &w) {
+                                              T m, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
     if (!(con.dist < T(0))) return;                 // collision.py:74 (NaN fails too)
     if (absval(con.dist) < p.thr) return;           // collision.py:79-80
     const V3<T> r = {con.pos.x - x.x, con.pos.y - x.y, con.pos.z - x.z};   // :75
     T jn;
     V3<T> jt;
-    if (impulse(m, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI, r, n, jn, jt);
+    if (impulse(m, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
+}
+
+// K1 broadphase over the 2x2x2 nearest cells of the step-start snapshot.
+// Cell size = 2 x the largest contact reach (2 x max bounding diameter), so
+// every partner lies in this body's cell or the neighbour on the nearer side
+// along each axis.  All 8 bucket counts are loaded at once, then candidates
+// in batches of RB_QBATCH (entry loads in flight together).  Hits go to a
+// per-lane list in LDS kept in ascending body id (the canonical
+// Gauss-Seidel order); returns the list length.
+template <typename T, int MAXP>
+__device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
+                                                   T rad, T bi, int32_t *s_id, int32_t *s_ent, int tid) {
+    int32_t np_ = 0;
+    int32_t cx, cy, cz;
+    if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
+        atomicOr(p.err, ERR_DOMAIN);
+        return 0;
+    }
+    const int32_t sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
+    const int32_t sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
+    const int32_t sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
+    uint32_t b[8];
+    int32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid.hmask);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = p.cnt_cur[b[k]];
+    int32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int32_t n = c[k] < p.grid.cap ? c[k] : p.grid.cap;
+#pragma unroll
+        for (int j = 0; j < k; ++j)
+            if (b[j] == b[k]) n = 0;                  // two cells hashed to one bucket: visit once
+        c[k] = n;
+        total += n;
+    }
+    bool overflow = false;
+    for (int base = 0; base < total; base += RB_QBATCH) {
+        Entry<T> e[RB_QBATCH];
+        int32_t ea[RB_QBATCH];
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u) {
+            int32_t rem = base + u;
+            int64_t addr = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (rem >= 0 && rem < c[k]) addr = entry_index(b[k], rem, p.grid.cap);
+                rem -= c[k];
+            }
+            ea[u] = (int32_t)addr;
+            if (base + u < total) e[u] = p.ent_cur[addr];
+            else e[u].id = i;
+        }
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u) {
+            const int32_t j = e[u].id;
+            if (j == i) continue;
+            const V3<T> cj = {e[u].x, e[u].y, e[u].z};
+            if (kind != 0 || e[u].kind != 0) {
+                // box-involved pair: not restated
+                const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
+                if (sqroot(mj_dot(dd, dd)) <= bi + e[u].r) atomicOr(p.err, ERR_UNSUPPORTED);
+                continue;
+            }
+            if (!sphere_sphere_hit(x, rad, cj, e[u].r)) continue;
+            int pos = np_;
+            bool dup = false;
+            while (pos > 0) {
+                const int32_t prev = s_id[(pos - 1) * STEP_BLOCK + tid];
+                if (prev == j) { dup = true; break; }
+                if (prev < j) break;
+                --pos;
+            }
+            if (dup) continue;
+            if (np_ >= MAXP) { overflow = true; continue; }
+            for (int t = np_; t > pos; --t) {
+                s_id[t * STEP_BLOCK + tid] = s_id[(t - 1) * STEP_BLOCK + tid];
+                s_ent[t * STEP_BLOCK + tid] = s_ent[(t - 1) * STEP_BLOCK + tid];
+            }
+            s_id[pos * STEP_BLOCK + tid] = j;
+            s_ent[pos * STEP_BLOCK + tid] = ea[u];
+            ++np_;
+        }
+    }
+    if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
+    return np_;
 }
 
 template <typename T, int MAXP>
@@ -93,6 +250,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     __shared__ int32_t s_ent[MAXP * STEP_BLOCK];
     const int tid = threadIdx.x;
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
+    STAMP(0);
 
     // the table of step t+2 was last read by step t-1: clear it for t+1's inserts
     for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
@@ -100,33 +258,39 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     const int32_t l = (int32_t)gt;
     const int32_t i = p.lo + l;
 
-    // ---- load (coalesced SoA) --------------------------------------------
+    // ---- K1 first: the contact search reads only step-start data -----------
     V3<T> x = {p.st.px[l], p.st.py[l], p.st.pz[l]};
+    const int32_t kind = p.cs.kind[i];
+    const T bi = p.cs.bound[i];
+    const V3<T> sz = {p.cs.sx[i], p.cs.sy[i], p.cs.sz[i]};
+    STAMP(1);
+    const int32_t np_ = (RB_ABLATE == 1) ? 0 : search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, s_ent, tid);
+    STAMP(2);
+
+    // ---- state (coalesced SoA) ----------------------------------------------
     const Q4<T> q = {p.st.qw[l], p.st.qx[l], p.st.qy[l], p.st.qz[l]};
     V3<T> v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
     V3<T> w = {p.st.wx[l], p.st.wy[l], p.st.wz[l]};
     const T m = p.cs.mass[i];
-    const V3<T> I = {p.cs.ix[i], p.cs.iy[i], p.cs.iz[i]};
-    const int32_t kind = p.cs.kind[i];
-    const V3<T> sz = {p.cs.sx[i], p.cs.sy[i], p.cs.sz[i]};
+    LazyInvI<T> invI;
+    invI.I = {p.cs.ix[i], p.cs.iy[i], p.cs.iz[i]};
+    invI.q = q;
 
-    // ---- a3 + a4: world inertia, gravity / applied force -----------------
-    const M3<T> invI = np_inv3(inertia_world(I, q));                  // collision.py:62, :70
+    // ---- a4: gravity / applied force (collision.py:66-70) ------------------
     {
-        V3<T> F = {m * p.g[0], m * p.g[1], m * p.g[2]};                // :66
-        if (p.xfrc) {
-            F = {p.xfrc[l] + F.x, p.xfrc[p.S + l] + F.y, p.xfrc[2 * p.S + l] + F.z};
-        }
-        v = {v.x + (F.x / m) * p.dt, v.y + (F.y / m) * p.dt, v.z + (F.z / m) * p.dt};   // :69
+        V3<T> F = {m * p.g[0], m * p.g[1], m * p.g[2]};
+        if (p.xfrc) F = {p.xfrc[l] + F.x, p.xfrc[p.S + l] + F.y, p.xfrc[2 * p.S + l] + F.z};
+        v = {v.x + (F.x / m) * p.dt, v.y + (F.y / m) * p.dt, v.z + (F.z / m) * p.dt};
         if (p.xfrc) {
             const V3<T> tdt = {p.xfrc[3 * p.S + l] * p.dt, p.xfrc[4 * p.S + l] * p.dt, p.xfrc[5 * p.S + l] * p.dt};
-            const V3<T> dw = np_matvec(invI, tdt);
+            const V3<T> dw = np_matvec(invI.get(), tdt);
             w = {w.x + dw.x, w.y + dw.y, w.z + dw.z};
         }
     }
 
+    STAMP(3);
     int32_t nrec = 0;
-    // ---- K1+K2: plane contacts, plane order --------------------------------
+    // ---- K2: plane contacts, plane order -------------------------------------
     if (kind == 0) {
         for (int pl = 0; pl < p.n_planes; ++pl) {
             const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
@@ -153,95 +317,59 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
         }
     }
 
-    // ---- K1: broadphase over the 27 neighbour cells of the snapshot --------
-    int32_t np_ = 0;
-    bool overflow = false;
-    {
-        int32_t cx, cy, cz;
-        if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
-            atomicOr(p.err, ERR_DOMAIN);
-        } else {
-            const T bi = p.cs.bound[i];
-            for (int dz = -1; dz <= 1; ++dz)
-                for (int dy = -1; dy <= 1; ++dy)
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const uint32_t b = cell_hash<T>(cx + dx, cy + dy, cz + dz) & p.grid.hmask;
-                        int32_t nb = p.cnt_cur[b];
-                        nb = nb < p.grid.cap ? nb : p.grid.cap;
-                        const int64_t base = (int64_t)b * p.grid.cap;
-                        for (int s = 0; s < nb; ++s) {
-                            const Entry<T> e = p.ent_cur[base + s];
-                            const int32_t j = e.id;
-                            if (j == i) continue;
-                            const V3<T> cj = {e.x, e.y, e.z};
-                            if (kind != 0 || p.cs.kind[j] != 0) {
-                                // box-involved pair: not restated
-                                const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
-                                if (sqroot(mj_dot(dd, dd)) <= bi + p.cs.bound[j]) atomicOr(p.err, ERR_UNSUPPORTED);
-                                continue;
-                            }
-                            if (!sphere_sphere_hit(x, sz.x, cj, p.cs.sx[j])) continue;
-                            // insert into the ascending-id list (dedupe: a bucket can
-                            // be reached from two neighbour cells after hashing)
-                            int pos = np_;
-                            bool dup = false;
-                            while (pos > 0) {
-                                const int32_t prev = s_id[(pos - 1) * STEP_BLOCK + tid];
-                                if (prev == j) { dup = true; break; }
-                                if (prev < j) break;
-                                --pos;
-                            }
-                            if (dup) continue;
-                            if (np_ >= MAXP) { overflow = true; continue; }
-                            for (int t = np_; t > pos; --t) {
-                                s_id[t * STEP_BLOCK + tid] = s_id[(t - 1) * STEP_BLOCK + tid];
-                                s_ent[t * STEP_BLOCK + tid] = s_ent[(t - 1) * STEP_BLOCK + tid];
-                            }
-                            s_id[pos * STEP_BLOCK + tid] = j;
-                            s_ent[pos * STEP_BLOCK + tid] = (int32_t)(base + s);
-                            ++np_;
-                        }
-                    }
+    // ---- K2: sphere partners in ascending id order ---------------------------
+    // (partner snapshots re-read 4 at a time — L1/L2-hot from the search;
+    // the solve itself is the reference's sequential Gauss-Seidel)
+    for (int s0 = 0; s0 < np_; s0 += 4) {
+        Entry<T> pe[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (s0 + u < np_) pe[u] = p.ent_cur[s_ent[(s0 + u) * STEP_BLOCK + tid]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (s0 + u >= np_) break;
+            const int32_t j = s_id[(s0 + u) * STEP_BLOCK + tid];
+            const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};
+            const T rj = pe[u].r;
+            Contact<T> con;
+            V3<T> n;
+            if (i < j) {                        // this body is geom1
+                sphere_sphere(x, sz.x, cj, rj, con);
+                n = p.oriented ? V3<T>{-con.frame.x, -con.frame.y, -con.frame.z} : con.frame;
+            } else {
+                sphere_sphere(cj, rj, x, sz.x, con);
+                n = con.frame;
+            }
+            record(p, l, nrec, j, 16, con.dist);
+            solve_contact(p, con, x, n, m, invI, v, w);
         }
-    }
-    if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
-
-    // ---- K2: sphere partners in ascending id order -------------------------
-    for (int s = 0; s < np_; ++s) {
-        const int32_t j = s_id[s * STEP_BLOCK + tid];
-        const Entry<T> e = p.ent_cur[s_ent[s * STEP_BLOCK + tid]];
-        const V3<T> cj = {e.x, e.y, e.z};
-        const T rj = p.cs.sx[j];
-        Contact<T> con;
-        V3<T> n;
-        if (i < j) {                        // this body is geom1
-            sphere_sphere(x, sz.x, cj, rj, con);
-            n = p.oriented ? V3<T>{-con.frame.x, -con.frame.y, -con.frame.z} : con.frame;
-        } else {
-            sphere_sphere(cj, rj, x, sz.x, con);
-            n = con.frame;
-        }
-        record(p, l, nrec, j, 16, con.dist);
-        solve_contact(p, con, x, n, m, invI, v, w);
     }
     if (p.rec_count) p.rec_count[l] = nrec;
+    STAMP(4);
 
-    // ---- K3: integrate (collision.py:90-100) -------------------------------
+    // ---- K3: integrate (collision.py:90-100) ---------------------------------
     x = {x.x + v.x * p.dt, x.y + v.y * p.dt, x.z + v.z * p.dt};
+    p.st.px[l] = x.x; p.st.py[l] = x.y; p.st.pz[l] = x.z;
+    // next step's broadphase snapshot: issue the slot atomic now so its
+    // round trip overlaps the quaternion update
+    if (p.cnt_next) insert_body(p.grid, p.cnt_next, p.ent_next, p.err, x.x, x.y, x.z, bi, i, kind);
+    STAMP(5);
     const Q4<T> res = mj_mulquat(Q4<T>{T(0), w.x, w.y, w.z}, q);
     Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
                 q.y + (T(0.5) * res.y) * p.dt, q.z + (T(0.5) * res.z) * p.dt};
     const T nq = sqroot(fmadd(qn.z, qn.z, fmadd(qn.y, qn.y, fmadd(qn.x, qn.x, qn.w * qn.w))));
     qn = {qn.w / nq, qn.x / nq, qn.y / nq, qn.z / nq};
-
-    p.st.px[l] = x.x; p.st.py[l] = x.y; p.st.pz[l] = x.z;
     p.st.qw[l] = qn.w; p.st.qx[l] = qn.x; p.st.qy[l] = qn.y; p.st.qz[l] = qn.z;
     p.st.vx[l] = v.x; p.st.vy[l] = v.y; p.st.vz[l] = v.z;
     p.st.wx[l] = w.x; p.st.wy[l] = w.y; p.st.wz[l] = w.z;
-
-    // ---- next step's broadphase snapshot ----------------------------------
-    if (p.cnt_next) insert_body(p.grid, p.cnt_next, p.ent_next, p.err, x.x, x.y, x.z, i);
+    STAMP(6);
 }
+
+#if RB_STAMPS
+extern "C" int rb_diag_stamps(unsigned long long *out, int nblocks) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 8 * nblocks);
+}
+#endif
 
 // ---- known-answer kernels ----------------------------------------------
 template <typename T>

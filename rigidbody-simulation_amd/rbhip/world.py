@@ -18,7 +18,7 @@ from .scenes import Scene
 
 class World:
     def __init__(self, scene: Scene, device: int = 0, dtype: str = "f64", rank: int = 0,
-                 world_size: int = 1, max_partners: int = 16, bucket_capacity: int = 16,
+                 world_size: int = 1, max_partners: int = 16, bucket_capacity: int = 0,
                  normal_convention: Optional[str] = None):
         L = _lib.load()
         self.scene = scene
