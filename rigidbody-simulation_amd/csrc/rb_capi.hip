@@ -10,6 +10,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -68,6 +69,7 @@ struct rb_world {
     int64_t N = 0, S = 0, Npad = 0, lo = 0;
     int32_t n_local = 0, P = 1, rank = 0;
     int32_t n_planes = 0, oriented = 1, maxp = 16, cap = 16, maxrec = 0;
+    int64_t coop_max = 32768;   // owned bodies up to which the cooperative search is used
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};
     double inv_cs = 1.0;
@@ -181,12 +183,12 @@ int launch_one(rb_world *w, hipStream_t s, int ph, double dt, double e, double m
         StepParams<double> p = make_step<double>(w, dt, e, mu, thr);
         set_tables(w, p, ph);
         if (!insert_next) { p.cnt_next = nullptr; p.ent_next = nullptr; }
-        r = launch_step<double>(p, w->maxp, s);
+        r = launch_step<double>(p, w->maxp, w->n_local <= w->coop_max, s);
     } else {
         StepParams<float> p = make_step<float>(w, dt, e, mu, thr);
         set_tables(w, p, ph);
         if (!insert_next) { p.cnt_next = nullptr; p.ent_next = nullptr; }
-        r = launch_step<float>(p, w->maxp, s);
+        r = launch_step<float>(p, w->maxp, w->n_local <= w->coop_max, s);
     }
     HIPCHK(r);
     return RB_OK;
@@ -416,6 +418,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxp = maxp;
     w->cap = d->bucket_capacity > 0 ? d->bucket_capacity : 16;
     w->maxrec = 4 * w->n_planes + w->maxp;
+    if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     // buckets: >= 4 per body and >= 256 tiles of 256 (spatially coherent
     // tiles are hashed; keep tile collisions rare)
 #ifndef RB_HMULT

@@ -87,7 +87,7 @@ template <typename T> struct InsertParams {
 };
 
 // launchers (rb_kernels.hip)
-template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, hipStream_t s);
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, bool coop, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s);

@@ -166,6 +166,7 @@ __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Cont
 template <typename T, int MAXP>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                    T rad, T bi, int32_t *s_id, int32_t *s_ent, int tid) {
+    constexpr int NB = STEP_BLOCK;      // one body per lane
     int32_t np_ = 0;
     int32_t cx, cy, cz;
     if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
@@ -224,7 +225,7 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
             int pos = np_;
             bool dup = false;
             while (pos > 0) {
-                const int32_t prev = s_id[(pos - 1) * STEP_BLOCK + tid];
+                const int32_t prev = s_id[(pos - 1) * NB + tid];
                 if (prev == j) { dup = true; break; }
                 if (prev < j) break;
                 --pos;
@@ -232,11 +233,11 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
             if (dup) continue;
             if (np_ >= MAXP) { overflow = true; continue; }
             for (int t = np_; t > pos; --t) {
-                s_id[t * STEP_BLOCK + tid] = s_id[(t - 1) * STEP_BLOCK + tid];
-                s_ent[t * STEP_BLOCK + tid] = s_ent[(t - 1) * STEP_BLOCK + tid];
+                s_id[t * NB + tid] = s_id[(t - 1) * NB + tid];
+                s_ent[t * NB + tid] = s_ent[(t - 1) * NB + tid];
             }
-            s_id[pos * STEP_BLOCK + tid] = j;
-            s_ent[pos * STEP_BLOCK + tid] = ea[u];
+            s_id[pos * NB + tid] = j;
+            s_ent[pos * NB + tid] = ea[u];
             ++np_;
         }
     }
@@ -244,29 +245,97 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
     return np_;
 }
 
-template <typename T, int MAXP>
-__global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
-    __shared__ int32_t s_id[MAXP * STEP_BLOCK];
-    __shared__ int32_t s_ent[MAXP * STEP_BLOCK];
-    const int tid = threadIdx.x;
-    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
-    STAMP(0);
+// Cooperative K1 for small scenes: G lanes per body, lane k of the group owns
+// neighbour cell k of the 2x2x2 neighbourhood (its count and candidates are
+// fetched in parallel with the other cells').  Hits become a bitmask over the
+// cell's slots; a group prefix sum (shuffles) places them in LDS, and the
+// group rank-sorts them by body id.  Same contact set and order as
+// search_partners — only the work distribution differs.
+template <typename T, int MAXP, int G>
+__device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
+                                               V3<T> x, T rad, T bi, int32_t *s_id, int32_t *s_ent, int32_t *t_id,
+                                               int32_t *t_ent, int slot, int k, int lane) {
+    static_assert(G == 8, "one lane per neighbour cell");
+    constexpr int NB = STEP_BLOCK / G;
+    int32_t cx = 0, cy = 0, cz = 0;
+    bool ok = active;
+    if (active && !cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
+        if (k == 0) atomicOr(p.err, ERR_DOMAIN);
+        ok = false;
+    }
+    const int32_t sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
+    const int32_t sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
+    const int32_t sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
+    const uint32_t b = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0),
+                                 p.grid.hmask);
+    int32_t c = ok ? p.cnt_cur[b] : 0;
+    c = c < p.grid.cap ? c : p.grid.cap;
+    const int gbase = lane & ~(G - 1);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const uint32_t bj = (uint32_t)__shfl((int)b, gbase + j);
+        if (j < k && bj == b) c = 0;                  // bucket already visited by a lower cell
+    }
+    uint32_t mask = 0;
+    for (int s0 = 0; s0 < c; s0 += RB_QBATCH) {
+        Entry<T> e[RB_QBATCH];
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u) {
+            if (s0 + u < c) e[u] = p.ent_cur[entry_index(b, s0 + u, p.grid.cap)];
+            else e[u].id = i;
+        }
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u) {
+            const int32_t j = e[u].id;
+            if (j == i) continue;
+            const V3<T> cj = {e[u].x, e[u].y, e[u].z};
+            if (kind != 0 || e[u].kind != 0) {
+                const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
+                if (sqroot(mj_dot(dd, dd)) <= bi + e[u].r) atomicOr(p.err, ERR_UNSUPPORTED);
+                continue;
+            }
+            if (sphere_sphere_hit(x, rad, cj, e[u].r)) mask |= 1u << (s0 + u);
+        }
+    }
+    const int h = __popc(mask);
+    int pre = 0, total = 0;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        const int hj = __shfl(h, gbase + j);
+        total += hj;
+        if (j < k) pre += hj;
+    }
+    if (total > MAXP && k == 0) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
+    int o = pre;
+    while (mask) {
+        const int sl = __builtin_ctz(mask);
+        mask &= mask - 1;
+        if (o < MAXP) {
+            const int64_t addr = entry_index(b, sl, p.grid.cap);
+            t_id[slot * MAXP + o] = p.ent_cur[addr].id;
+            t_ent[slot * MAXP + o] = (int32_t)addr;
+        }
+        ++o;
+    }
+    __syncthreads();
+    const int tot = total < MAXP ? total : MAXP;
+    for (int qq = k; qq < tot; qq += G) {
+        const int32_t id = t_id[slot * MAXP + qq];
+        int r = 0;
+        for (int j = 0; j < tot; ++j) r += t_id[slot * MAXP + j] < id;
+        s_id[r * NB + slot] = id;
+        s_ent[r * NB + slot] = t_ent[slot * MAXP + qq];
+    }
+    __syncthreads();
+    return tot;
+}
 
-    // the table of step t+2 was last read by step t-1: clear it for t+1's inserts
-    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
-    if (gt >= p.n_local) return;
-    const int32_t l = (int32_t)gt;
-    const int32_t i = p.lo + l;
-
-    // ---- K1 first: the contact search reads only step-start data -----------
-    V3<T> x = {p.st.px[l], p.st.py[l], p.st.pz[l]};
-    const int32_t kind = p.cs.kind[i];
-    const T bi = p.cs.bound[i];
-    const V3<T> sz = {p.cs.sx[i], p.cs.sy[i], p.cs.sz[i]};
-    STAMP(1);
-    const int32_t np_ = (RB_ABLATE == 1) ? 0 : search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, s_ent, tid);
-    STAMP(2);
-
+// Everything after the contact search for one body (lane): gravity, the
+// Gauss-Seidel solves in canonical order, integration, next-step insert.
+template <typename T, int MAXP, int NB>
+__device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
+                                            V3<T> sz, T bi, int32_t np_, const int32_t *s_id, const int32_t *s_ent,
+                                            int slot, int tid) {
     // ---- state (coalesced SoA) ----------------------------------------------
     const Q4<T> q = {p.st.qw[l], p.st.qx[l], p.st.qy[l], p.st.qz[l]};
     V3<T> v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
@@ -324,11 +393,11 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
         Entry<T> pe[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (s0 + u < np_) pe[u] = p.ent_cur[s_ent[(s0 + u) * STEP_BLOCK + tid]];
+            if (s0 + u < np_) pe[u] = p.ent_cur[s_ent[(s0 + u) * NB + slot]];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (s0 + u >= np_) break;
-            const int32_t j = s_id[(s0 + u) * STEP_BLOCK + tid];
+            const int32_t j = s_id[(s0 + u) * NB + slot];
             const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};
             const T rj = pe[u].r;
             Contact<T> con;
@@ -363,6 +432,42 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     p.st.vx[l] = v.x; p.st.vy[l] = v.y; p.st.vz[l] = v.z;
     p.st.wx[l] = w.x; p.st.wy[l] = w.y; p.st.wz[l] = w.z;
     STAMP(6);
+}
+
+template <typename T, int MAXP, int G>
+__global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
+    constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
+    __shared__ int32_t s_id[MAXP * NB];
+    __shared__ int32_t s_ent[MAXP * NB];
+    __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
+    __shared__ int32_t t_ent[G > 1 ? MAXP * NB : 1];
+    const int tid = threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
+    STAMP(0);
+
+    // the table of step t+2 was last read by step t-1: clear it for t+1's inserts
+    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
+    const int slot = tid / G, k = tid % G;
+    const int64_t lb = (int64_t)blockIdx.x * NB + slot;
+    const bool active = lb < p.n_local;
+    if (G == 1 && !active) return;
+    const int32_t l = active ? (int32_t)lb : 0;
+    const int32_t i = p.lo + l;
+
+    // ---- K1 first: the contact search reads only step-start data -----------
+    const V3<T> x = {p.st.px[l], p.st.py[l], p.st.pz[l]};
+    const int32_t kind = p.cs.kind[i];
+    const T bi = p.cs.bound[i];
+    const V3<T> sz = {p.cs.sx[i], p.cs.sy[i], p.cs.sz[i]};
+    STAMP(1);
+    int32_t np_ = 0;
+    if (RB_ABLATE != 1) {
+        if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, s_ent, tid);
+        else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_ent, t_id, t_ent, slot, k, tid);
+    }
+    STAMP(2);
+    if (!active || k != 0) return;
+    body_update<T, MAXP, NB>(p, l, i, x, kind, sz, bi, np_, s_id, s_ent, slot, tid);
 }
 
 #if RB_STAMPS
@@ -420,13 +525,17 @@ __global__ void kat_apply_kernel(int64_t n, const double *in, double *out) {
 }
 
 // ---- launchers ----------------------------------------------------------
-template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, hipStream_t s) {
-    const int64_t work = p.n_local > p.grid.H ? p.n_local : p.grid.H;
-    int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, bool coop, hipStream_t s) {
+    const int nb = coop ? STEP_BLOCK / 8 : STEP_BLOCK;
+    int64_t blocks = (p.n_local + nb - 1) / nb;
     if (blocks < 1) blocks = 1;
-    (void)work;
-    if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-    else hipLaunchKernelGGL((step_kernel<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    if (coop) {
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16, 8>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((step_kernel<T, 32, 8>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    } else {
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16, 1>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((step_kernel<T, 32, 1>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    }
     return hipGetLastError();
 }
 
@@ -457,8 +566,8 @@ template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, d
 
 template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);
-template hipError_t launch_step<double>(const StepParams<double> &, int, hipStream_t);
-template hipError_t launch_step<float>(const StepParams<float> &, int, hipStream_t);
+template hipError_t launch_step<double>(const StepParams<double> &, int, bool, hipStream_t);
+template hipError_t launch_step<float>(const StepParams<float> &, int, bool, hipStream_t);
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
 template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
 template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *, hipStream_t);

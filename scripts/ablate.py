@@ -1,34 +1,41 @@
-"""Diagnostic: build RB_ABLATE variants of librbhip.so and time the step
-kernel (HIP events per launch) on several scene sizes, interleaved in one
-process.  Not part of the product; results go to stdout."""
-import os, subprocess, sys, json
+"""Diagnostic: time the step kernel (HIP events per launch) for several
+builds (VARIANTS: ";"-separated extra compiler flags) and runtime settings
+(ENVS: ";"-separated NAME=VALUE applied before each world is created), over
+several flat-sphere scene sizes, interleaved in one process.  Not part of the
+product; results go to stdout."""
+import os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rigidbody-simulation_amd"))
 CSRC = os.path.join(ROOT, "rigidbody-simulation_amd", "csrc")
-# VARIANTS: ";"-separated lists of extra compiler flags, one build each
-variants = os.environ.get("VARIANTS", "-DRB_ABLATE=0;-DRB_ABLATE=1").split(";")
+variants = os.environ.get("VARIANTS", "").split(";")
+envs = os.environ.get("ENVS", "").split(";")
+sizes = [tuple(int(v) for v in s.split("x")) for s in os.environ.get("SIZES", "64x64,256x256,1024x1024").split(",")]
 paths = {}
 for k, v in enumerate(variants):
     out = f"/tmp/librbhip_ablate{k}.so"
     subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
                    f"{v} -o {out} rb_kernels.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
     paths[v] = out
-import ctypes
 from rbhip import _lib, scenes
 import rbhip.world as W
-sizes = [(64, 64), (256, 256), (1024, 1024)]
 res = {}
 for rnd in range(2):
     for v in variants:
         _lib._lib = None
         _lib.load(paths[v])
-        for nx, ny in sizes:
-            sc = scenes.flat_spheres(nx, ny, seed=0)
-            with W.World(sc) as w:
-                w.step(60)
-                w.kernel_timing(True)
-                w.step(100)
-                avg, n = w.kernel_timing(False)
-            res.setdefault((v, nx * ny), []).append(avg)
-for (v, n), t in sorted(res.items()):
-    print(f"variant {v:24s} N={n:8d}  step kernel ms: {min(t):.4f}  ->  {n / min(t) / 1e6:.1f} G body-steps/s (kernel only)")
+        for env in envs:
+            if env:
+                name, val = env.split("=")
+                os.environ[name] = val
+            for nx, ny in sizes:
+                sc = scenes.flat_spheres(nx, ny, seed=0)
+                with W.World(sc) as w:
+                    w.step(60)
+                    w.kernel_timing(True)
+                    w.step(100)
+                    avg, n = w.kernel_timing(False)
+                res.setdefault((v, env, nx * ny), []).append(avg)
+            if env:
+                del os.environ[env.split("=")[0]]
+for (v, env, n), t in sorted(res.items(), key=lambda kv: (kv[0][2], kv[0][0], kv[0][1])):
+    print(f"N={n:8d} {v:20s} {env:34s} kernel ms {min(t):.4f} -> {n / min(t) / 1e6:7.2f} G body-steps/s")

@@ -128,22 +128,32 @@ def test_f32_bit_exact_vs_f32_restatement(rb, oracle):
     assert np.array_equal(q, q0) and np.array_equal(v, v0)
 
 
-def test_f32_vs_f64_tolerance_sweep(rb):
-    """C3 sweep: fp32 stays close to fp64 over a short horizon."""
+def test_f32_vs_f64_tolerance_sweep(rb, oracle):
+    """C3 fp32-vs-fp64 sweep (SURVEY §8d, §7 hard part 5): from the same
+    evolved fp64 state, one step in each precision — contact flips (pairs
+    present in one list only) and the one-step state error; the long-horizon
+    divergence is reported, not asserted (contacts decided differently send
+    chaotic bodies on other trajectories)."""
     from rbhip import scenes
     sc = scenes.make("c3")
-    out = {}
+    q, v = oracle.step(oracle.OracleScene(sc), sc.qpos0, sc.qvel0, 30)
+    res = {}
     for dt in ("f64", "f32"):
-        with rb.World(sc, dtype=dt) as w:
-            w.step(100)
-            out[dt] = w.get_state()[0]
-    d = np.abs(out["f32"][:, :3] - out["f64"][:, :3])
-    rel = d / (1.0 + np.abs(out["f64"][:, :3]))
-    # fp32 carries ~1e-7 relative per operation on coordinates up to ~40 m;
-    # a contact decided differently (flip) sends a few bodies on another
-    # trajectory — reported, not asserted exact (SURVEY §7 hard part 5)
-    diverged = (d.max(axis=1) > 1e-2).mean()
-    assert np.median(rel) < 5e-5 and diverged < 0.02, (np.median(rel), diverged)
+        with rb.World(sc.with_(qpos0=q, qvel0=v), dtype=dt) as w:
+            w.record_contacts(True)
+            w.step(1)
+            qq, vv = w.get_state()
+            cnt, par, kin, dis = w.contacts()
+        body = np.repeat(np.arange(sc.n), cnt)
+        res[dt] = (qq, vv, set(zip(body.tolist(), par.tolist())))
+    flips = len(res["f64"][2] ^ res["f32"][2])
+    ncon = len(res["f64"][2])
+    d = np.abs(res["f32"][0][:, :3] - res["f64"][0][:, :3])
+    rel = d / (1.0 + np.abs(res["f64"][0][:, :3]))
+    print(f"\nC3 fp32 vs fp64, one step from step 30: {ncon} contacts, {flips} flips, "
+          f"median rel dpos {np.median(rel):.2e}, max |dpos| {d.max():.2e}")
+    assert ncon > 1000 and flips <= max(2, ncon // 1000)
+    assert np.median(rel) < 1e-6 and d.max() < 1e-3
 
 
 def test_xfrc_applied_matches_oracle(rb, oracle):
