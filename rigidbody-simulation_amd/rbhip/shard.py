@@ -49,10 +49,14 @@ class ShardedWorld:
 
     transport: "nccl" (RCCL all-gather on device memory; the default when the
     process group backend is nccl) or "host" (stage through host memory, for
-    gloo process groups, e.g. several ranks sharing one GPU in tests)."""
+    gloo process groups, e.g. several ranks sharing one GPU in tests).
+
+    `world_factory(rank, world_size)` may supply the per-rank stepper (any
+    object with the World shard interface and a `gpos_tensor(torch)`
+    method); by default it is a HIP World on `device`."""
 
     def __init__(self, scene: Scene, dtype: str = "f64", device: Optional[int] = None,
-                 group=None, transport: Optional[str] = None, **world_kw):
+                 group=None, transport: Optional[str] = None, world_factory=None, **world_kw):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -62,15 +66,19 @@ class ShardedWorld:
             backend = dist.get_backend(group)
         else:
             self.rank, self.P, backend = 0, 1, None
-        if device is None:
-            device = torch.cuda.current_device()
-        torch.cuda.set_device(device)
         self.transport = transport or ("nccl" if backend == "nccl" else "host")
-        self.world = World(scene, device=device, dtype=dtype, rank=self.rank, world_size=self.P,
-                           **world_kw)
-        self.stream = torch.cuda.current_stream(device)
-        self.world.set_stream(self.stream.cuda_stream)
-        self.gpos, self.shard_elems = wrap_gpos(self.world, torch)
+        if world_factory is not None:
+            self.world = world_factory(self.rank, self.P)
+            self.gpos, self.shard_elems = self.world.gpos_tensor(torch)
+        else:
+            if device is None:
+                device = torch.cuda.current_device()
+            torch.cuda.set_device(device)
+            self.world = World(scene, device=device, dtype=dtype, rank=self.rank, world_size=self.P,
+                               **world_kw)
+            self.stream = torch.cuda.current_stream(device)
+            self.world.set_stream(self.stream.cuda_stream)
+            self.gpos, self.shard_elems = wrap_gpos(self.world, torch)
         self.mine = self.gpos[self.rank * self.shard_elems:(self.rank + 1) * self.shard_elems]
 
     def _exchange(self):
@@ -103,6 +111,8 @@ class ShardedWorld:
         t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
         if self.transport == "nccl":
             t = t.to(self.gpos.device)
+        elif t.dtype != self.torch.float64:
+            t = t.double()
         self.dist.all_reduce(t, group=self.group)      # rows are disjoint: sum == union
         a = t.cpu().numpy()
         return a[:, :7].copy(), a[:, 7:].copy()
