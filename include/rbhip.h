@@ -93,8 +93,10 @@ void rb_world_destroy(rb_world *w);
 const char *rb_last_error(void);
 const char *rb_version(void);
 
-/* Bind the world to a caller-owned HIP stream (hipStream_t; NULL = the
- * world's own stream).  All later work of this world is enqueued there. */
+/* Bind the world to a caller-owned HIP stream (hipStream_t; NULL is HIP's
+ * default null stream, e.g. torch's default stream).  Until this is called
+ * the world uses a private non-blocking stream.  All later work of this
+ * world is enqueued on the bound stream. */
 int rb_set_stream(rb_world *w, void *hip_stream);
 
 /* ---- state transfer (the only AoS<->SoA transposes) --------------------- */

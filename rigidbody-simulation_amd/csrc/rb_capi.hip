@@ -468,7 +468,7 @@ void rb_world_destroy(rb_world *w) { free_world(w); }
 
 int rb_set_stream(rb_world *w, void *s) {
     if (!w) return fail(RB_EINVAL, "null world");
-    w->stream = s ? (hipStream_t)s : w->own_stream;
+    w->stream = (hipStream_t)s;        // NULL = HIP's null stream
     return RB_OK;
 }
 

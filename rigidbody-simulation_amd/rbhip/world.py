@@ -92,6 +92,8 @@ class World:
         _lib.check(self._L.rb_set_xfrc(self._h, _lib.ptr(x)), "rb_set_xfrc")
 
     def set_stream(self, stream_handle: int):
+        """Enqueue all later work on this hipStream_t (0 = HIP's null stream,
+        which is torch's default stream)."""
         _lib.check(self._L.rb_set_stream(self._h, C.c_void_p(stream_handle or None)), "rb_set_stream")
 
     # ---- stepping -----------------------------------------------------------
