@@ -71,7 +71,7 @@ typedef struct rb_scene_desc {
     int32_t rank;              /* shard index: owns bodies [rank*S, rank*S+S) ∩ [0,N)  */
     int32_t world_size;        /* shard count P; S = ceil(N / P)                       */
     int32_t max_partners;      /* sphere-sphere contacts per body (0 = default 16)     */
-    int32_t bucket_capacity;   /* broadphase bodies per hash bucket (0 = default 16)   */
+    int32_t bucket_capacity;   /* reserved: broadphase ids per cell bucket are 32      */
     const int32_t *kind;       /* [N]   RB_BODY_*                                      */
     const double  *mass;       /* [N]   model.body_mass of each free body              */
     const double  *inertia;    /* [N*3] model.body_inertia (principal, body frame)     */
@@ -132,16 +132,20 @@ int rb_step_async(rb_world *w, int64_t nsteps, double dt, double restitution,
 int rb_sync(rb_world *w);
 
 /* ---- sharded stepping (world_size > 1) ---------------------------------- */
-/* One step of the owned bodies; new owned positions land in the replicated
- * position buffer.  The caller then all-gathers that buffer (RCCL over
- * xGMI via torch.distributed, or any transport) and calls
- * rb_shard_exchange_done, which publishes the other ranks' positions to the
- * broadphase.  Both calls are enqueued only. */
+/* One step of the owned bodies; their new positions land in this rank's
+ * slice of the replicated position buffer of the next step.  The caller then
+ * all-gathers that buffer (RCCL over xGMI via torch.distributed, or any
+ * transport) and calls rb_shard_exchange_done, which publishes the other
+ * ranks' positions to the next step's broadphase.  Both calls are enqueued
+ * only. */
 int rb_shard_step(rb_world *w, double dt, double restitution, double friction,
                   double contact_threshold);
 int rb_shard_exchange_done(rb_world *w);
-/* Device view of the replicated position buffer: layout [P][3][S] of the
- * world's dtype; this rank's slice is [rank][3][S] (contiguous 3*S elems). */
+/* Device view of the position buffer the pending exchange fills (valid
+ * between rb_shard_step and rb_shard_exchange_done; two buffers alternate
+ * step by step).  Layout [P][S][4] of the world's dtype — (x, y, z,
+ * bounding radius) per body, bodies in global id order; this rank's slice
+ * is the contiguous [rank][S][4] (shard_elems = 4*S elements). */
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems,
                    int32_t *elem_bytes);
 

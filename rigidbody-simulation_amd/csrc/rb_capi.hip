@@ -1,10 +1,12 @@
 // rb_capi.hip — implementation of include/rbhip.h.
 //
-// A world owns its device buffers (struct-of-arrays state, replicated
-// constants, three rotating broadphase tables) and enqueues all work on one
-// HIP stream.  Multi-step calls on a single shard are captured once into a
-// hipGraph (one kernel node per step) and replayed, so K steps cost one host
-// submission.
+// A world owns its device buffers — struct-of-arrays state, replicated
+// constants, two ping-pong position snapshots (which double as the
+// replicated exchange buffer of sharded worlds) and three rotating
+// broadphase tables — and enqueues all work on one HIP stream.  A step's
+// buffers are fixed by the step counter modulo 6 (tables mod 3, snapshots
+// mod 2), so multi-step calls on a single shard are captured once per
+// phase into a hipGraph (one kernel node per step) and replayed.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -57,7 +59,7 @@ int err_to_code(int32_t bits) {
     if (bits & ERR_UNSUPPORTED)
         return fail(RB_EUNSUPPORTED, "device: box-box / box-sphere pair within contact range (not restated)");
     if (bits & ERR_PARTNER_OVERFLOW) return fail(RB_EOVERFLOW, "device: a body has more sphere partners than max_partners");
-    if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: broadphase bucket capacity exceeded");
+    if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: more than 32 bodies hashed to one broadphase cell");
     return RB_OK;
 }
 
@@ -68,29 +70,29 @@ struct rb_world {
     hipStream_t stream = nullptr, own_stream = nullptr, cap_stream = nullptr;
     int64_t N = 0, S = 0, Npad = 0, lo = 0;
     int32_t n_local = 0, P = 1, rank = 0;
-    int32_t n_planes = 0, oriented = 1, maxp = 16, cap = 16, maxrec = 0;
+    int32_t n_planes = 0, oriented = 1, maxp = 16, maxrec = 0;
     int64_t coop_max = 32768;   // owned bodies up to which the cooperative search is used
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};
     double inv_cs = 1.0;
-    int64_t H = 1024;
+    int64_t H = 4096;
     int64_t bytes_per_body_step = 0;
     // device memory
-    void *gpos = nullptr;      // [P][3][S]
+    void *snap[2] = {};        // [Npad] Snap<T>: (x, y, z, bound radius), ping-pong
     void *state = nullptr;     // 10 x S  (qw qx qy qz vx vy vz wx wy wz)
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
-    int32_t *cnt[3] = {};
-    void *ent[3] = {};
+    int32_t *cnt[3] = {};      // [H] broadphase bucket counts
+    uint32_t *ids[3] = {};     // [H][BUCKET_SLOTS] broadphase bucket ids
     int32_t *err = nullptr;
     int32_t *err_host = nullptr;   // pinned
     // recording
     bool record = false;
     int32_t *rec_count = nullptr, *rec_partner = nullptr, *rec_kind = nullptr;
     void *rec_dist = nullptr;
-    // stepping state
-    int phase = 0;
+    // stepping state: step counter c; tables rotate mod 3, snapshots mod 2
+    int64_t c = 0;
     bool primed = false;
     std::map<std::tuple<int64_t, int, double, double, double, double, int>, hipGraphExec_t> graphs;
     // kernel timing
@@ -98,27 +100,40 @@ struct rb_world {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
     double t_sum_ms = 0;
     int64_t t_n = 0;
+
+    int phase() const { return (int)(c % 3); }
+    int sp() const { return (int)(c % 2); }
 };
 
 namespace {
 
 template <typename T> T *dp(void *p, int64_t off) { return reinterpret_cast<T *>(p) + off; }
 
-template <typename T> StepParams<T> make_step(rb_world *w, double dt, double e, double mu, double thr) {
+template <typename T> Grid<T> make_grid(const rb_world *w) {
+    Grid<T> g;
+    g.inv_cs = (T)w->inv_cs;
+    g.hmask = (uint32_t)(w->H - 1);
+    g.H = (int32_t)w->H;
+    return g;
+}
+
+Table table(const rb_world *w, int k) { return Table{w->cnt[k], w->ids[k]}; }
+
+// parameters of the step with counter value c
+template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt, double e, double mu, double thr,
+                                              bool insert_next) {
     StepParams<T> p{};
     p.n_global = w->N;
     p.n_local = w->n_local;
     p.lo = (int32_t)w->lo;
     p.S = (int32_t)w->S;
-    T *gp = dp<T>(w->gpos, (int64_t)w->rank * 3 * w->S);
-    p.st.px = gp; p.st.py = gp + w->S; p.st.pz = gp + 2 * w->S;
     T *st = dp<T>(w->state, 0);
     T **f[10] = {&p.st.qw, &p.st.qx, &p.st.qy, &p.st.qz, &p.st.vx, &p.st.vy, &p.st.vz, &p.st.wx, &p.st.wy, &p.st.wz};
     for (int k = 0; k < 10; ++k) *f[k] = st + k * w->S;
-    const T *c = dp<T>(w->consts, 0);
-    p.cs.mass = c; p.cs.ix = c + w->Npad; p.cs.iy = c + 2 * w->Npad; p.cs.iz = c + 3 * w->Npad;
-    p.cs.sx = c + 4 * w->Npad; p.cs.sy = c + 5 * w->Npad; p.cs.sz = c + 6 * w->Npad;
-    p.cs.bound = c + 7 * w->Npad;
+    const T *cst = dp<T>(w->consts, 0);
+    p.cs.mass = cst; p.cs.ix = cst + w->Npad; p.cs.iy = cst + 2 * w->Npad; p.cs.iz = cst + 3 * w->Npad;
+    p.cs.sx = cst + 4 * w->Npad; p.cs.sy = cst + 5 * w->Npad; p.cs.sz = cst + 6 * w->Npad;
+    p.cs.bound = cst + 7 * w->Npad;
     p.cs.kind = w->kind;
     p.xfrc = w->xfrc ? dp<T>(w->xfrc, 0) : nullptr;
     p.n_planes = w->n_planes;
@@ -127,10 +142,13 @@ template <typename T> StepParams<T> make_step(rb_world *w, double dt, double e, 
     for (int d = 0; d < 3; ++d) p.g[d] = (T)w->g[d];
     p.dt = (T)dt; p.e = (T)e; p.mu = (T)mu; p.thr = (T)thr;
     p.oriented = w->oriented;
-    p.grid.inv_cs = (T)w->inv_cs;
-    p.grid.hmask = (uint32_t)(w->H - 1);
-    p.grid.cap = w->cap;
-    p.grid.H = (int32_t)w->H;
+    p.grid = make_grid<T>(w);
+    const int ph = (int)(c % 3), sp = (int)(c % 2);
+    p.snap_cur = dp<Snap<T>>(w->snap[sp], 0);
+    p.snap_next = dp<Snap<T>>(w->snap[1 - sp], 0);
+    p.cur = table(w, ph);
+    p.next = insert_next ? table(w, (ph + 1) % 3) : Table{nullptr, nullptr};
+    p.cnt_clear = w->cnt[(ph + 2) % 3];
     p.err = w->err;
     if (w->record) {
         p.rec_count = w->rec_count; p.rec_partner = w->rec_partner; p.rec_kind = w->rec_kind;
@@ -140,56 +158,34 @@ template <typename T> StepParams<T> make_step(rb_world *w, double dt, double e, 
     return p;
 }
 
-template <typename T> void set_tables(rb_world *w, StepParams<T> &p, int ph) {
-    p.cnt_cur = w->cnt[ph];
-    p.ent_cur = dp<Entry<T>>(w->ent[ph], 0);
-    p.cnt_next = w->cnt[(ph + 1) % 3];
-    p.ent_next = dp<Entry<T>>(w->ent[(ph + 1) % 3], 0);
-    p.cnt_clear = w->cnt[(ph + 2) % 3];
-}
-
-template <typename T> InsertParams<T> make_insert(rb_world *w, int ph, int64_t first, int64_t count,
+template <typename T> InsertParams<T> make_insert(rb_world *w, int sp, int ph, int64_t first, int64_t count,
                                                   int64_t skip_lo, int64_t skip_hi) {
     InsertParams<T> ip{};
-    ip.gpos = dp<T>(w->gpos, 0);
-    ip.bound = dp<T>(w->consts, 7 * w->Npad);
+    ip.snap = dp<Snap<T>>(w->snap[sp], 0);
     ip.kind = w->kind;
-    ip.S = (int32_t)w->S;
     ip.first = first; ip.count = count; ip.skip_lo = skip_lo; ip.skip_hi = skip_hi;
-    ip.grid.inv_cs = (T)w->inv_cs;
-    ip.grid.hmask = (uint32_t)(w->H - 1);
-    ip.grid.cap = w->cap;
-    ip.grid.H = (int32_t)w->H;
-    ip.cnt = w->cnt[ph];
-    ip.ent = dp<Entry<T>>(w->ent[ph], 0);
+    ip.grid = make_grid<T>(w);
+    ip.tab = table(w, ph);
     ip.err = w->err;
     return ip;
 }
 
-// (re)build the current table from every body's position
+// (re)build the current table from every body's snapshot
 int prime(rb_world *w) {
     for (int k = 0; k < 3; ++k) HIPCHK(hipMemsetAsync(w->cnt[k], 0, sizeof(int32_t) * w->H, w->stream));
     hipError_t e = w->dtype == RB_F64
-                       ? launch_insert<double>(make_insert<double>(w, w->phase, 0, w->N, 0, 0), w->stream)
-                       : launch_insert<float>(make_insert<float>(w, w->phase, 0, w->N, 0, 0), w->stream);
+                       ? launch_insert<double>(make_insert<double>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream)
+                       : launch_insert<float>(make_insert<float>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream);
     HIPCHK(e);
     w->primed = true;
     return RB_OK;
 }
 
-int launch_one(rb_world *w, hipStream_t s, int ph, double dt, double e, double mu, double thr, bool insert_next) {
+int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, double mu, double thr) {
     hipError_t r;
-    if (w->dtype == RB_F64) {
-        StepParams<double> p = make_step<double>(w, dt, e, mu, thr);
-        set_tables(w, p, ph);
-        if (!insert_next) { p.cnt_next = nullptr; p.ent_next = nullptr; }
-        r = launch_step<double>(p, w->maxp, w->n_local <= w->coop_max, s);
-    } else {
-        StepParams<float> p = make_step<float>(w, dt, e, mu, thr);
-        set_tables(w, p, ph);
-        if (!insert_next) { p.cnt_next = nullptr; p.ent_next = nullptr; }
-        r = launch_step<float>(p, w->maxp, w->n_local <= w->coop_max, s);
-    }
+    const bool coop = w->n_local <= w->coop_max;
+    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, coop, s);
+    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, coop, s);
     HIPCHK(r);
     return RB_OK;
 }
@@ -221,35 +217,45 @@ int collect_timing(rb_world *w) {
     return RB_OK;
 }
 
+int timed_launch(rb_world *w, double dt, double e, double mu, double thr) {
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, w->stream));
+    int rc = launch_one(w, w->stream, w->c, dt, e, mu, thr);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(b, w->stream));
+    w->tev.emplace_back(a, b);
+    if (w->tev.size() >= 4096) return collect_timing(w);
+    return RB_OK;
+}
+
+void drop_graphs(rb_world *w) {
+    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+    w->graphs.clear();
+}
+
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
     if (w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_step + exchange");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0))
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
-    hipError_t se = hipSetDevice(w->device);
-    HIPCHK(se);
+    HIPCHK(hipSetDevice(w->device));
     if (!w->primed) { int rc = prime(w); if (rc) return rc; }
     if (w->timing) {
         // eager launches, each bracketed by events on the launch stream
         for (int64_t k = 0; k < nsteps; ++k) {
-            hipEvent_t a, b;
-            HIPCHK(hipEventCreate(&a));
-            HIPCHK(hipEventCreate(&b));
-            HIPCHK(hipEventRecord(a, w->stream));
-            int rc = launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+            int rc = timed_launch(w, dt, e, mu, thr);
             if (rc) return rc;
-            HIPCHK(hipEventRecord(b, w->stream));
-            w->tev.emplace_back(a, b);
-            w->phase = (w->phase + 1) % 3;
-            if (w->tev.size() >= 4096) { int rc2 = collect_timing(w); if (rc2) return rc2; }
+            ++w->c;
         }
         return RB_OK;
     }
     if (nsteps == 1) {
-        int rc = launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+        int rc = launch_one(w, w->stream, w->c, dt, e, mu, thr);
         if (rc) return rc;
-        w->phase = (w->phase + 1) % 3;
+        ++w->c;
         return RB_OK;
     }
     // K > 1: replay a captured graph of K step nodes
@@ -257,46 +263,40 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     int64_t left = nsteps;
     while (left > 0) {
         const int64_t K = left > chunk_max ? chunk_max : left;
-        auto key = std::make_tuple(K, w->phase, dt, e, mu, thr, (int)w->record);
+        auto key = std::make_tuple(K, (int)(w->c % 6), dt, e, mu, thr, (int)w->record);
         auto it = w->graphs.find(key);
         if (it == w->graphs.end()) {
-            if (w->graphs.size() >= 30) {
-                for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
-                w->graphs.clear();
-            }
-            // capture the three table-phase variants at once, so later calls
+            if (w->graphs.size() >= 60) drop_graphs(w);
+            // capture the six buffer-phase variants at once, so later calls
             // starting at any phase replay without a capture
-            for (int ph0 = 0; ph0 < 3; ++ph0) {
+            for (int c0 = 0; c0 < 6; ++c0) {
                 hipGraph_t graph;
                 hipGraphExec_t ex;
                 HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
-                int ph = ph0;
                 for (int64_t k = 0; k < K; ++k) {
-                    int rc = launch_one(w, w->cap_stream, ph, dt, e, mu, thr, true);
+                    int rc = launch_one(w, w->cap_stream, c0 + k, dt, e, mu, thr);
                     if (rc) { (void)hipStreamEndCapture(w->cap_stream, &graph); return rc; }
-                    ph = (ph + 1) % 3;
                 }
                 HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
                 HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
                 (void)hipGraphDestroy(graph);
-                w->graphs[std::make_tuple(K, ph0, dt, e, mu, thr, (int)w->record)] = ex;
+                w->graphs[std::make_tuple(K, c0, dt, e, mu, thr, (int)w->record)] = ex;
             }
             it = w->graphs.find(key);
         }
-        hipGraphExec_t exec = it->second;
-        HIPCHK(hipGraphLaunch(exec, w->stream));
-        w->phase = (int)((w->phase + K) % 3);
+        HIPCHK(hipGraphLaunch(it->second, w->stream));
+        w->c += K;
         left -= K;
     }
     return RB_OK;
 }
 
 template <typename T>
-int upload_state(rb_world *w, const double *qpos, const double *qvel) {
-    std::vector<T> g((size_t)w->P * 3 * w->S, T(0));
+int upload_state(rb_world *w, const double *qpos, const double *qvel, const double *bound) {
+    std::vector<T> sn((size_t)4 * w->Npad, T(0));
     for (int64_t b = 0; b < w->N; ++b) {
-        const int64_t r = b / w->S, l = b % w->S;
-        for (int d = 0; d < 3; ++d) g[(size_t)(r * 3 * w->S + d * w->S + l)] = (T)qpos[7 * b + d];
+        for (int d = 0; d < 3; ++d) sn[(size_t)(4 * b + d)] = (T)qpos[7 * b + d];
+        sn[(size_t)(4 * b + 3)] = (T)bound[b];
     }
     std::vector<T> st((size_t)10 * w->S, T(0));
     for (int64_t l = 0; l < w->n_local; ++l) {
@@ -304,7 +304,7 @@ int upload_state(rb_world *w, const double *qpos, const double *qvel) {
         for (int d = 0; d < 4; ++d) st[(size_t)(d * w->S + l)] = (T)qpos[7 * b + 3 + d];
         for (int d = 0; d < 6; ++d) st[(size_t)((4 + d) * w->S + l)] = (T)qvel[6 * b + d];
     }
-    HIPCHK(hipMemcpyAsync(w->gpos, g.data(), sizeof(T) * g.size(), hipMemcpyHostToDevice, w->stream));
+    HIPCHK(hipMemcpyAsync(w->snap[w->sp()], sn.data(), sizeof(T) * sn.size(), hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(w->state, st.data(), sizeof(T) * st.size(), hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
     return RB_OK;
@@ -312,15 +312,15 @@ int upload_state(rb_world *w, const double *qpos, const double *qvel) {
 
 template <typename T>
 int download_state(rb_world *w, double *qpos, double *qvel) {
-    std::vector<T> g((size_t)3 * w->S), st((size_t)10 * w->S);
-    HIPCHK(hipMemcpyAsync(g.data(), dp<T>(w->gpos, (int64_t)w->rank * 3 * w->S), sizeof(T) * g.size(),
+    std::vector<T> sn((size_t)4 * w->S), st((size_t)10 * w->S);
+    HIPCHK(hipMemcpyAsync(sn.data(), dp<T>(w->snap[w->sp()], 4 * w->lo), sizeof(T) * sn.size(),
                           hipMemcpyDeviceToHost, w->stream));
     HIPCHK(hipMemcpyAsync(st.data(), w->state, sizeof(T) * st.size(), hipMemcpyDeviceToHost, w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
     for (int64_t l = 0; l < w->n_local; ++l) {
         const int64_t b = w->lo + l;
         if (qpos) {
-            for (int d = 0; d < 3; ++d) qpos[7 * b + d] = (double)g[(size_t)(d * w->S + l)];
+            for (int d = 0; d < 3; ++d) qpos[7 * b + d] = (double)sn[(size_t)(4 * l + d)];
             for (int d = 0; d < 4; ++d) qpos[7 * b + 3 + d] = (double)st[(size_t)(d * w->S + l)];
         }
         if (qvel)
@@ -329,20 +329,26 @@ int download_state(rb_world *w, double *qpos, double *qvel) {
     return RB_OK;
 }
 
+double bound_of(const rb_scene_desc *d, int64_t b) {
+    const double *s = d->size + 3 * b;
+    return d->kind[b] == RB_BODY_SPHERE ? s[0] : sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+}
+
 template <typename T>
-int upload_consts(rb_world *w, const rb_scene_desc *d) {
+int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &bound) {
     std::vector<T> c((size_t)8 * w->Npad, T(0));
     double rmax = 0;
+    bound.assign((size_t)w->N, 0.0);
     for (int64_t b = 0; b < w->N; ++b) {
         const double *s = d->size + 3 * b;
-        const double bound = d->kind[b] == RB_BODY_SPHERE ? s[0] : sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
-        if (bound > rmax) rmax = bound;
+        bound[(size_t)b] = bound_of(d, b);
+        if (bound[(size_t)b] > rmax) rmax = bound[(size_t)b];
         c[(size_t)(0 * w->Npad + b)] = (T)d->mass[b];
         for (int k = 0; k < 3; ++k) {
             c[(size_t)((1 + k) * w->Npad + b)] = (T)d->inertia[3 * b + k];
             c[(size_t)((4 + k) * w->Npad + b)] = (T)s[k];
         }
-        c[(size_t)(7 * w->Npad + b)] = (T)bound;
+        c[(size_t)(7 * w->Npad + b)] = (T)bound[(size_t)b];
     }
     // cell = 2 x the largest contact reach (2 x 2 rmax): the 2x2x2 query
     const double cs = rmax > 0 ? 4.0 * rmax * 1.001 : 1.0;
@@ -357,10 +363,10 @@ int upload_consts(rb_world *w, const rb_scene_desc *d) {
 void free_world(rb_world *w) {
     if (!w) return;
     (void)hipSetDevice(w->device);
-    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+    drop_graphs(w);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *bufs[] = {w->gpos, w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
-                    w->ent[0], w->ent[1], w->ent[2], w->err, w->rec_count, w->rec_partner, w->rec_kind,
+    void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
+                    w->ids[0], w->ids[1], w->ids[2], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -370,12 +376,15 @@ void free_world(rb_world *w) {
     delete w;
 }
 
+// host-side copy of the bounding radii (needed by rb_set_state)
+std::map<const rb_world *, std::vector<double>> g_bounds;
+
 }  // namespace
 
 extern "C" {
 
 const char *rb_last_error(void) { return g_err.c_str(); }
-const char *rb_version(void) { return "librbhip 0.1 (gfx950, HIP)"; }
+const char *rb_version(void) { return "librbhip 0.2 (gfx950, HIP)"; }
 
 int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (!out || !d) return fail(RB_EINVAL, "null argument");
@@ -390,6 +399,8 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         return fail(RB_EINVAL, "bad normal_convention");
     const int maxp = d->max_partners > 0 ? d->max_partners : 16;
     if (maxp > 32) return fail(RB_EINVAL, "max_partners must be <= 32");
+    if (d->bucket_capacity < 0 || d->bucket_capacity > BUCKET_SLOTS)
+        return fail(RB_EINVAL, "bucket_capacity must be <= %d", BUCKET_SLOTS);
     for (int64_t b = 0; b < d->n_bodies; ++b) {
         if (d->kind[b] != RB_BODY_SPHERE && d->kind[b] != RB_BODY_BOX) return fail(RB_EINVAL, "body %lld: bad kind", (long long)b);
         if (!(d->mass[b] > 0)) return fail(RB_EINVAL, "body %lld: mass must be > 0", (long long)b);
@@ -416,15 +427,10 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     for (int j = 0; j < 3; ++j) w->g[j] = d->gravity[j];
     w->oriented = d->normal_convention == RB_NORMAL_ORIENTED;
     w->maxp = maxp;
-    w->cap = d->bucket_capacity > 0 ? d->bucket_capacity : 16;
     w->maxrec = 4 * w->n_planes + w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
-    // buckets: >= 4 per body and >= 256 tiles of 256 (spatially coherent
-    // tiles are hashed; keep tile collisions rare)
-#ifndef RB_HMULT
-#define RB_HMULT 4
-#endif
-    w->H = next_pow2(RB_HMULT * w->N > 65536 ? RB_HMULT * w->N : 65536);
+    // per-cell hash: >= 4 buckets per body (occupied cells <= bodies)
+    w->H = next_pow2(4 * w->N > 4096 ? 4 * w->N : 4096);
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
     // algorithmic bytes per body-step: 13 state reals read + 13
@@ -438,14 +444,13 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         if (hipMalloc((void **)&(ptr), (bytes)) != hipSuccess)                                   \
             return bail(fail(RB_ENOMEM, "hipMalloc(%lld) failed", (long long)(bytes)));          \
     } while (0)
-    ALLOC(w->gpos, (size_t)w->esz * 3 * w->Npad);
+    for (int k = 0; k < 2; ++k) ALLOC(w->snap[k], (size_t)w->esz * 4 * w->Npad);
     ALLOC(w->state, (size_t)w->esz * 10 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
-    const size_t entsz = w->dtype == RB_F64 ? sizeof(Entry<double>) : sizeof(Entry<float>);
     for (int k = 0; k < 3; ++k) {
         ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
-        ALLOC(w->ent[k], entsz * w->H * w->cap);
+        ALLOC(w->ids[k], sizeof(uint32_t) * BUCKET_SLOTS * w->H);
     }
     ALLOC(w->err, sizeof(int32_t));
 #undef ALLOC
@@ -454,17 +459,23 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         hipStreamCreateWithFlags(&w->cap_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipStreamCreate failed"));
     w->stream = w->own_stream;
-    if (hipMemset(w->gpos, 0, (size_t)w->esz * 3 * w->Npad) != hipSuccess ||
+    if (hipMemset(w->snap[0], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
+        hipMemset(w->snap[1], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
         hipMemset(w->state, 0, (size_t)w->esz * 10 * w->S) != hipSuccess ||
         hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipMemset failed"));
-    int rc = w->dtype == RB_F64 ? upload_consts<double>(w, d) : upload_consts<float>(w, d);
+    std::vector<double> bound;
+    int rc = w->dtype == RB_F64 ? upload_consts<double>(w, d, bound) : upload_consts<float>(w, d, bound);
     if (rc) return bail(rc);
+    g_bounds[w] = std::move(bound);
     *out = w;
     return RB_OK;
 }
 
-void rb_world_destroy(rb_world *w) { free_world(w); }
+void rb_world_destroy(rb_world *w) {
+    g_bounds.erase(w);
+    free_world(w);
+}
 
 int rb_set_stream(rb_world *w, void *s) {
     if (!w) return fail(RB_EINVAL, "null world");
@@ -475,7 +486,9 @@ int rb_set_stream(rb_world *w, void *s) {
 int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     if (!w || !qpos || !qvel) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
-    int rc = w->dtype == RB_F64 ? upload_state<double>(w, qpos, qvel) : upload_state<float>(w, qpos, qvel);
+    const std::vector<double> &bound = g_bounds[w];
+    int rc = w->dtype == RB_F64 ? upload_state<double>(w, qpos, qvel, bound.data())
+                                : upload_state<float>(w, qpos, qvel, bound.data());
     w->primed = false;
     return rc;
 }
@@ -489,10 +502,9 @@ int rb_get_state(rb_world *w, double *qpos, double *qvel) {
 int rb_set_xfrc(rb_world *w, const double *xf) {
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
+    drop_graphs(w);
     if (!xf) {
         if (w->xfrc) { HIPCHK(hipFree(w->xfrc)); w->xfrc = nullptr; }
-        for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
-        w->graphs.clear();
         return RB_OK;
     }
     if (!w->xfrc) HIPCHK(hipMalloc(&w->xfrc, (size_t)w->esz * 6 * w->S));
@@ -505,8 +517,6 @@ int rb_set_xfrc(rb_world *w, const double *xf) {
         std::vector<float> f(h.begin(), h.end());
         HIPCHK(hipMemcpy(w->xfrc, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice));
     }
-    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
-    w->graphs.clear();
     return RB_OK;
 }
 
@@ -532,39 +542,28 @@ int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0)) return fail(RB_EINVAL, "invalid step parameters");
     HIPCHK(hipSetDevice(w->device));
     if (!w->primed) { int rc = prime(w); if (rc) return rc; }
-    if (w->timing) {
-        hipEvent_t a, b;
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
-        HIPCHK(hipEventRecord(a, w->stream));
-        int rc = launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(b, w->stream));
-        w->tev.emplace_back(a, b);
-        if (w->tev.size() >= 4096) { int rc2 = collect_timing(w); if (rc2) return rc2; }
-        return RB_OK;
-    }
-    return launch_one(w, w->stream, w->phase, dt, e, mu, thr, true);
+    if (w->timing) return timed_launch(w, dt, e, mu, thr);
+    return launch_one(w, w->stream, w->c, dt, e, mu, thr);
 }
 
 int rb_shard_exchange_done(rb_world *w) {
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
-    const int nph = (w->phase + 1) % 3;
     // insert every body not owned here into the next table (own ones went in
-    // from the step kernel)
+    // from the step kernel), reading the freshly exchanged snapshot
+    const int nsp = 1 - w->sp(), nph = (w->phase() + 1) % 3;
     hipError_t e = w->dtype == RB_F64
-                       ? launch_insert<double>(make_insert<double>(w, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream)
-                       : launch_insert<float>(make_insert<float>(w, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream);
+                       ? launch_insert<double>(make_insert<double>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream)
+                       : launch_insert<float>(make_insert<float>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream);
     HIPCHK(e);
-    w->phase = nph;
+    ++w->c;
     return RB_OK;
 }
 
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
     if (!w) return fail(RB_EINVAL, "null world");
-    if (dev_ptr) *dev_ptr = w->gpos;
-    if (shard_elems) *shard_elems = 3 * w->S;
+    if (dev_ptr) *dev_ptr = w->snap[1 - w->sp()];
+    if (shard_elems) *shard_elems = 4 * w->S;
     if (elem_bytes) *elem_bytes = w->esz;
     return RB_OK;
 }

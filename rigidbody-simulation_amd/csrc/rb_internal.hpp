@@ -15,19 +15,29 @@ enum : int32_t {
     ERR_DOMAIN = 8,             // non-finite / out-of-range position
 };
 
-// Broadphase bucket entry: a snapshot of a body's step-start position plus
-// what a candidate test needs (bounding radius == sphere radius for spheres,
-// body kind), so the query reads nothing else by body id.
-template <typename T> struct Entry;
-template <> struct alignas(16) Entry<double> { double x, y, z, r; int32_t id, kind; int32_t pad[2]; };
-template <> struct alignas(16) Entry<float> { float x, y, z, r; int32_t id, kind; int32_t pad[2]; };
+// Step-start snapshot of one body, indexed by global body id: position and
+// bounding radius (== the radius for a sphere).  Two snapshot buffers
+// ping-pong: a step reads one and writes the other, so every contact test
+// sees step-start positions (Jacobi across bodies, multi_sphere_bounce.py:43-46).
+// The buffer is also the replicated position buffer of sharded worlds:
+// layout [P][S][4], rank r's bodies are the contiguous slice [r*S, r*S+S).
+template <typename T> struct alignas(4 * sizeof(T)) Snap { T x, y, z, r; };
+
+// Broadphase buckets: per-cell hash -> a count and a 128-byte line of body
+// ids.  A body claims its slot with one atomicAdd on the count; counts are
+// cleared two steps ahead by the step kernel's grid (ids are never cleared).
+constexpr int BUCKET_SLOTS = 32;
+constexpr uint32_t BOX_FLAG = 0x80000000u;   // set on ids of box bodies
+struct Table {
+    int32_t *cnt;              // [H]
+    uint32_t *ids;             // [H][BUCKET_SLOTS]
+};
 
 constexpr int MAX_PLANES = 8;
 
-// Structure-of-arrays body state.  Positions live in the replicated
-// [P][3][S] buffer (this rank's slice = px/py/pz); the rest is per shard.
+// Structure-of-arrays body state of this shard (positions live in the
+// snapshots).
 template <typename T> struct BodyState {
-    T *px, *py, *pz;
     T *qw, *qx, *qy, *qz;
     T *vx, *vy, *vz;
     T *wx, *wy, *wz;
@@ -44,7 +54,6 @@ template <typename T> struct BodyConsts {
 template <typename T> struct Grid {
     T inv_cs;                          // 1 / cell size
     uint32_t hmask;                    // H - 1 (H power of two)
-    int32_t cap;                       // entries per bucket
     int32_t H;
 };
 
@@ -61,11 +70,11 @@ template <typename T> struct StepParams {
     T dt, e, mu, thr;
     int32_t oriented;
     Grid<T> grid;
-    const int32_t *cnt_cur;
-    const Entry<T> *ent_cur;
-    int32_t *cnt_next;
-    Entry<T> *ent_next;
-    int32_t *cnt_clear;
+    const Snap<T> *snap_cur;           // step-start snapshot (read)
+    Snap<T> *snap_next;                // next step's snapshot (own rows written)
+    Table cur;                         // broadphase of snap_cur
+    Table next;                        // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
+    int32_t *cnt_clear;                // counts of the table two steps ahead
     int32_t *err;
     // optional contact recording ([n_local][maxrec] slots)
     int32_t *rec_count, *rec_partner, *rec_kind;
@@ -74,15 +83,12 @@ template <typename T> struct StepParams {
 };
 
 template <typename T> struct InsertParams {
-    const T *gpos;                     // [P][3][S]
-    const T *bound;                    // [Npad] bounding radius
+    const Snap<T> *snap;               // [Npad]
     const int32_t *kind;               // [Npad]
-    int32_t S;
     int64_t first, count;              // global ids [first, first+count)
     int64_t skip_lo, skip_hi;          // global ids to skip (already inserted)
     Grid<T> grid;
-    int32_t *cnt;
-    Entry<T> *ent;
+    Table tab;
     int32_t *err;
 };
 

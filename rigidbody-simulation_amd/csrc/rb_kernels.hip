@@ -1,22 +1,25 @@
 // rb_kernels.hip — the hot path on gfx950.
 //
-// One launch per simulation step (rb::step_kernel), one thread per owned
-// body, 64-thread workgroups (one wave):
+// One launch per simulation step (rb::step_kernel), 64-thread workgroups
+// (one wave):
 //   K1 contact generation  — plane-sphere / plane-box corners against the
-//      static planes, sphere-sphere against the broadphase snapshot of the
-//      step-start positions (spatial-hash buckets of the 27 neighbour cells);
-//      partners are kept in a per-lane sorted list in LDS (ascending body id
-//      = the canonical Gauss-Seidel order, SURVEY §7 hard part 1);
+//      static planes; sphere-sphere against the step-start snapshot through
+//      a spatial hash of cells (2 x 2 x 2 nearest cells).  Partners go to a
+//      per-body list in LDS in ascending body id = the canonical
+//      Gauss-Seidel order (SURVEY §7 hard part 1).  Small scenes search
+//      cooperatively (8 lanes per body, one per cell), large ones one lane
+//      per body.
 //   K2 impulse solve       — per contact, in list order:
 //      compute_collision_impulse_friction (collision.py:7-48) then
 //      apply_impulse_friction (physics_utils.py:25-49);
 //   K3 integrate           — x += v dt, q += 0.5 (0,w)*q dt, normalise
-//      (collision.py:90-95), write SoA state in place;
-//   and the next step's broadphase: the body inserts its new position into
-//   the next table (atomic bucket slot) while the table two steps ahead is
-//   cleared by the whole grid.  Three tables rotate, so a step reads only a
-//   snapshot no thread of the same launch writes: Jacobi across bodies
-//   exactly as multi_sphere_bounce.py:43-46 (one mj_forward per step).
+//      (collision.py:90-95): state written in place, the new position into
+//      the next snapshot;
+//   and the next step's broadphase: the body inserts its id into the next
+//   table while the grid clears the counts of the table two steps ahead.
+//   Three tables and two snapshots rotate, so a step reads only data no
+//   thread of the same launch writes: Jacobi across bodies, exactly as
+//   multi_sphere_bounce.py:43-46 (one mj_forward per step).
 #include "rb_device.hpp"
 #include "rb_internal.hpp"
 
@@ -42,37 +45,23 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][8];
 #else
 #define STAMP(k) do {} while (0)
 #endif
-// candidates whose entry loads are issued together
+// candidates whose snapshot loads are issued together
 #ifndef RB_QBATCH
 #define RB_QBATCH 4
 #endif
 
 namespace rb {
 
-// tile coordinate -> well-mixed 32-bit hash (murmur3 finaliser)
-__device__ __forceinline__ uint32_t tile_hash(int32_t ix, int32_t iy, int32_t iz) {
+// cell -> bucket: murmur3-finalised hash of the cell coordinates
+__device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, uint32_t hmask) {
     uint32_t h = (uint32_t)ix * 0x8da6b343u + (uint32_t)iy * 0xd8163841u + (uint32_t)iz * 0xcb1ab31fu;
     h ^= h >> 16; h *= 0x85ebca6bu;
     h ^= h >> 13; h *= 0xc2b2ae35u;
     h ^= h >> 16;
-    return h;
+    return h & hmask;
 }
 
-// Spatially coherent bucket of a cell: 8x8x4-cell tiles are contiguous runs
-// of 256 buckets (x fastest), whole tiles are hashed.  Neighbouring cells —
-// and so the queries of neighbouring bodies — share cache lines.
-__device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, uint32_t hmask) {
-    const uint32_t t = tile_hash(ix >> 3, iy >> 3, iz >> 2);
-    return ((t << 8) | ((uint32_t)(iz & 3) << 6) | ((uint32_t)(iy & 7) << 3) | (uint32_t)(ix & 7)) & hmask;
-}
-
-// Entries are slot-major within a tile: [tile][slot][256 cells], so the
-// first entries of adjacent cells are adjacent in memory.
-__device__ __forceinline__ int64_t entry_index(uint32_t b, int32_t slot, int32_t cap) {
-    return ((int64_t)(b >> 8) * cap + slot) * 256 + (b & 255u);
-}
-
-// cell coordinates; false (and ERR_DOMAIN) for non-finite / out-of-range
+// cell coordinates; false for non-finite / out-of-range positions
 template <typename T>
 __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, int32_t &iy, int32_t &iz) {
     const T fx = x * inv_cs, fy = y * inv_cs, fz = z * inv_cs;
@@ -84,17 +73,28 @@ __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, in
     return true;
 }
 
+// Append an id to the bucket of (x, y, z): one returning atomicAdd claims
+// the slot.
 template <typename T>
-__device__ __forceinline__ void insert_body(const Grid<T> &g, int32_t *cnt, Entry<T> *ent, int32_t *err,
-                                            T x, T y, T z, T r, int32_t id, int32_t kind) {
+__device__ __forceinline__ void insert_id(const Grid<T> &g, const Table &tab, int32_t *err, T x, T y, T z,
+                                          uint32_t tagged_id) {
     int32_t ix, iy, iz;
     if (!cell_of(x, y, z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return; }
     const uint32_t b = bucket_of(ix, iy, iz, g.hmask);
-    const int32_t slot = atomicAdd(cnt + b, 1);
-    if (slot >= g.cap) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    Entry<T> e;
-    e.x = x; e.y = y; e.z = z; e.r = r; e.id = id; e.kind = kind; e.pad[0] = 0; e.pad[1] = 0;
-    ent[entry_index(b, slot, g.cap)] = e;
+    const int32_t slot = atomicAdd(tab.cnt + b, 1);
+    if (slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    tab.ids[(int64_t)b * BUCKET_SLOTS + slot] = tagged_id;
+}
+
+// count (clamped) and the first 4 ids of a bucket, loaded together
+__device__ __forceinline__ uint4 bucket_head(const Table &tab, uint32_t b, int32_t &count) {
+    const int32_t c = tab.cnt[b];
+    const uint4 h = *reinterpret_cast<const uint4 *>(tab.ids + (int64_t)b * BUCKET_SLOTS);
+    count = c < BUCKET_SLOTS ? c : BUCKET_SLOTS;
+    return h;
+}
+__device__ __forceinline__ uint32_t bucket_id(const Table &tab, uint32_t b, const uint4 &h, int s) {
+    return s == 0 ? h.x : s == 1 ? h.y : s == 2 ? h.z : s == 3 ? h.w : tab.ids[(int64_t)b * BUCKET_SLOTS + s];
 }
 
 template <typename T>
@@ -103,10 +103,8 @@ __global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
     if (k >= p.count) return;
     const int64_t id = p.first + k;
     if (id >= p.skip_lo && id < p.skip_hi) return;
-    const int64_t r = id / p.S, l = id - r * p.S;
-    const T *base = p.gpos + r * 3 * (int64_t)p.S;
-    insert_body(p.grid, p.cnt, p.ent, p.err, base[l], base[p.S + l], base[2 * (int64_t)p.S + l], p.bound[id],
-                (int32_t)id, p.kind[id]);
+    const Snap<T> s = p.snap[id];
+    insert_id(p.grid, p.tab, p.err, s.x, s.y, s.z, (uint32_t)id | (p.kind[id] != 0 ? BOX_FLAG : 0u));
 }
 
 template <typename T>
@@ -156,120 +154,137 @@ __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Cont
     if (impulse(m, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
 }
 
-// K1 broadphase over the 2x2x2 nearest cells of the step-start snapshot.
-// Cell size = 2 x the largest contact reach (2 x max bounding diameter), so
-// every partner lies in this body's cell or the neighbour on the nearer side
-// along each axis.  All 8 bucket counts are loaded at once, then candidates
-// in batches of RB_QBATCH (entry loads in flight together).  Hits go to a
-// per-lane list in LDS kept in ascending body id (the canonical
-// Gauss-Seidel order); returns the list length.
+// Candidate test shared by both search forms: true if the candidate with
+// snapshot s and tagged id tj is a sphere partner of body i.
+template <typename T>
+__device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x, T rad, T bi,
+                                              uint32_t tj, const Snap<T> &s) {
+    const int32_t j = (int32_t)(tj & ~BOX_FLAG);
+    if (j == i) return false;
+    const V3<T> cj = {s.x, s.y, s.z};
+    if (kind != 0 || (tj & BOX_FLAG)) {
+        // box-involved pair: not restated
+        const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
+        if (sqroot(mj_dot(dd, dd)) <= bi + s.r) atomicOr(p.err, ERR_UNSUPPORTED);
+        return false;
+    }
+    return sphere_sphere_hit(x, rad, cj, s.r);
+}
+
+// The 2x2x2 cell neighbourhood: cell size = 2 x the largest contact reach
+// (2 x max bounding diameter), so every partner lies in this body's cell or
+// its neighbour on the nearer side along each axis.
+template <typename T>
+__device__ __forceinline__ bool neighbourhood(const StepParams<T> &p, V3<T> x, int32_t &cx, int32_t &cy, int32_t &cz,
+                                              int32_t &sx, int32_t &sy, int32_t &sz) {
+    if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) return false;
+    sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
+    sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
+    sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
+    return true;
+}
+
+// Insert partner id j into a per-body list kept ascending in LDS.
+template <int MAXP>
+__device__ __forceinline__ void list_insert(int32_t *s_id, int stride, int slot, int32_t &np_, int32_t j,
+                                            bool &overflow) {
+    int pos = np_;
+    while (pos > 0) {
+        const int32_t prev = s_id[(pos - 1) * stride + slot];
+        if (prev == j) return;                       // reached through two hashed cells
+        if (prev < j) break;
+        --pos;
+    }
+    if (np_ >= MAXP) { overflow = true; return; }
+    for (int t = np_; t > pos; --t) s_id[t * stride + slot] = s_id[(t - 1) * stride + slot];
+    s_id[pos * stride + slot] = j;
+    ++np_;
+}
+
+// K1, one lane per body: the 8 bucket counts and the first 4 ids of each
+// bucket are loaded together, then candidates in batches of RB_QBATCH
+// (snapshot loads in flight together).  Returns the partner count.
 template <typename T, int MAXP>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
-                                                   T rad, T bi, int32_t *s_id, int32_t *s_ent, int tid) {
-    constexpr int NB = STEP_BLOCK;      // one body per lane
-    int32_t np_ = 0;
-    int32_t cx, cy, cz;
-    if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
-        atomicOr(p.err, ERR_DOMAIN);
-        return 0;
-    }
-    const int32_t sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
-    const int32_t sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
-    const int32_t sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
+                                                   T rad, T bi, int32_t *s_id, int tid) {
+    constexpr int NB = STEP_BLOCK;
+    int32_t cx, cy, cz, sx, sy, sz;
+    if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) { atomicOr(p.err, ERR_DOMAIN); return 0; }
     uint32_t b[8];
     int32_t c[8];
+    uint4 id4[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid.hmask);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = p.cnt_cur[b[k]];
+    for (int k = 0; k < 8; ++k) id4[k] = bucket_head(p.cur, b[k], c[k]);
     int32_t total = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        int32_t n = c[k] < p.grid.cap ? c[k] : p.grid.cap;
+        int32_t n = c[k];
 #pragma unroll
         for (int j = 0; j < k; ++j)
             if (b[j] == b[k]) n = 0;                  // two cells hashed to one bucket: visit once
         c[k] = n;
         total += n;
     }
+    int32_t np_ = 0;
     bool overflow = false;
     for (int base = 0; base < total; base += RB_QBATCH) {
-        Entry<T> e[RB_QBATCH];
-        int32_t ea[RB_QBATCH];
+        uint32_t tj[RB_QBATCH];
+        Snap<T> sn[RB_QBATCH];
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u) {
             int32_t rem = base + u;
-            int64_t addr = 0;
+            uint32_t t = (uint32_t)i;
+            int64_t addr = -1;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (rem >= 0 && rem < c[k]) addr = entry_index(b[k], rem, p.grid.cap);
+                if (rem >= 0 && rem < c[k]) {
+                    if (rem == 0) t = id4[k].x;
+                    else if (rem == 1) t = id4[k].y;
+                    else if (rem == 2) t = id4[k].z;
+                    else if (rem == 3) t = id4[k].w;
+                    else addr = (int64_t)b[k] * BUCKET_SLOTS + rem;
+                }
                 rem -= c[k];
             }
-            ea[u] = (int32_t)addr;
-            if (base + u < total) e[u] = p.ent_cur[addr];
-            else e[u].id = i;
+            if (base + u < total && addr >= 0) t = p.cur.ids[addr];
+            tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
 #pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) {
-            const int32_t j = e[u].id;
-            if (j == i) continue;
-            const V3<T> cj = {e[u].x, e[u].y, e[u].z};
-            if (kind != 0 || e[u].kind != 0) {
-                // box-involved pair: not restated
-                const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
-                if (sqroot(mj_dot(dd, dd)) <= bi + e[u].r) atomicOr(p.err, ERR_UNSUPPORTED);
-                continue;
-            }
-            if (!sphere_sphere_hit(x, rad, cj, e[u].r)) continue;
-            int pos = np_;
-            bool dup = false;
-            while (pos > 0) {
-                const int32_t prev = s_id[(pos - 1) * NB + tid];
-                if (prev == j) { dup = true; break; }
-                if (prev < j) break;
-                --pos;
-            }
-            if (dup) continue;
-            if (np_ >= MAXP) { overflow = true; continue; }
-            for (int t = np_; t > pos; --t) {
-                s_id[t * NB + tid] = s_id[(t - 1) * NB + tid];
-                s_ent[t * NB + tid] = s_ent[(t - 1) * NB + tid];
-            }
-            s_id[pos * NB + tid] = j;
-            s_ent[pos * NB + tid] = ea[u];
-            ++np_;
-        }
+        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[tj[u] & ~BOX_FLAG];
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u)
+            if (candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u]))
+                list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
     }
     if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
     return np_;
 }
 
-// Cooperative K1 for small scenes: G lanes per body, lane k of the group owns
-// neighbour cell k of the 2x2x2 neighbourhood (its count and candidates are
-// fetched in parallel with the other cells').  Hits become a bitmask over the
-// cell's slots; a group prefix sum (shuffles) places them in LDS, and the
-// group rank-sorts them by body id.  Same contact set and order as
-// search_partners — only the work distribution differs.
+// K1 for small scenes: G lanes per body, lane k of the group owns neighbour
+// cell k (its count, ids and candidate snapshots are fetched in parallel
+// with the other cells').  Hits become a bitmask over the bucket slots; a
+// group prefix sum (shuffles) places them in LDS and the group rank-sorts
+// them by body id.  Same contact set and order as search_partners.
 template <typename T, int MAXP, int G>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
-                                               V3<T> x, T rad, T bi, int32_t *s_id, int32_t *s_ent, int32_t *t_id,
-                                               int32_t *t_ent, int slot, int k, int lane) {
+                                               V3<T> x, T rad, T bi, int32_t *s_id, int32_t *t_id, int slot, int k,
+                                               int lane) {
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
-    int32_t cx = 0, cy = 0, cz = 0;
+    int32_t cx = 0, cy = 0, cz = 0, sx = 1, sy = 1, sz = 1;
     bool ok = active;
-    if (active && !cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) {
+    if (active && !neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) {
         if (k == 0) atomicOr(p.err, ERR_DOMAIN);
         ok = false;
     }
-    const int32_t sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
-    const int32_t sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
-    const int32_t sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
     const uint32_t b = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0),
                                  p.grid.hmask);
-    int32_t c = ok ? p.cnt_cur[b] : 0;
-    c = c < p.grid.cap ? c : p.grid.cap;
+    int32_t c = 0;
+    uint4 id4 = {0, 0, 0, 0};
+    if (ok) id4 = bucket_head(p.cur, b, c);
     const int gbase = lane & ~(G - 1);
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -278,24 +293,20 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     }
     uint32_t mask = 0;
     for (int s0 = 0; s0 < c; s0 += RB_QBATCH) {
-        Entry<T> e[RB_QBATCH];
+        uint32_t tj[RB_QBATCH];
+        Snap<T> sn[RB_QBATCH];
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u) {
-            if (s0 + u < c) e[u] = p.ent_cur[entry_index(b, s0 + u, p.grid.cap)];
-            else e[u].id = i;
+            const int s = s0 + u;
+            uint32_t t = (uint32_t)i;
+            if (s < c) t = bucket_id(p.cur, b, id4, s);
+            tj[u] = t;
         }
 #pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) {
-            const int32_t j = e[u].id;
-            if (j == i) continue;
-            const V3<T> cj = {e[u].x, e[u].y, e[u].z};
-            if (kind != 0 || e[u].kind != 0) {
-                const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
-                if (sqroot(mj_dot(dd, dd)) <= bi + e[u].r) atomicOr(p.err, ERR_UNSUPPORTED);
-                continue;
-            }
-            if (sphere_sphere_hit(x, rad, cj, e[u].r)) mask |= 1u << (s0 + u);
-        }
+        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[tj[u] & ~BOX_FLAG];
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u)
+            if (candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
     }
     const int h = __popc(mask);
     int pre = 0, total = 0;
@@ -311,9 +322,8 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         const int sl = __builtin_ctz(mask);
         mask &= mask - 1;
         if (o < MAXP) {
-            const int64_t addr = entry_index(b, sl, p.grid.cap);
-            t_id[slot * MAXP + o] = p.ent_cur[addr].id;
-            t_ent[slot * MAXP + o] = (int32_t)addr;
+            const uint32_t t = bucket_id(p.cur, b, id4, sl);
+            t_id[slot * MAXP + o] = (int32_t)t;
         }
         ++o;
     }
@@ -324,7 +334,6 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         int r = 0;
         for (int j = 0; j < tot; ++j) r += t_id[slot * MAXP + j] < id;
         s_id[r * NB + slot] = id;
-        s_ent[r * NB + slot] = t_ent[slot * MAXP + qq];
     }
     __syncthreads();
     return tot;
@@ -334,8 +343,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
 // Gauss-Seidel solves in canonical order, integration, next-step insert.
 template <typename T, int MAXP, int NB>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
-                                            V3<T> sz, T bi, int32_t np_, const int32_t *s_id, const int32_t *s_ent,
-                                            int slot, int tid) {
+                                            V3<T> sz, T bi, int32_t np_, const int32_t *s_id, int slot, int tid) {
     // ---- state (coalesced SoA) ----------------------------------------------
     const Q4<T> q = {p.st.qw[l], p.st.qx[l], p.st.qy[l], p.st.qz[l]};
     V3<T> v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
@@ -390,10 +398,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // (partner snapshots re-read 4 at a time — L1/L2-hot from the search;
     // the solve itself is the reference's sequential Gauss-Seidel)
     for (int s0 = 0; s0 < np_; s0 += 4) {
-        Entry<T> pe[4];
+        Snap<T> pe[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (s0 + u < np_) pe[u] = p.ent_cur[s_ent[(s0 + u) * NB + slot]];
+            if (s0 + u < np_) pe[u] = p.snap_cur[s_id[(s0 + u) * NB + slot]];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (s0 + u >= np_) break;
@@ -418,10 +426,12 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 
     // ---- K3: integrate (collision.py:90-100) ---------------------------------
     x = {x.x + v.x * p.dt, x.y + v.y * p.dt, x.z + v.z * p.dt};
-    p.st.px[l] = x.x; p.st.py[l] = x.y; p.st.pz[l] = x.z;
-    // next step's broadphase snapshot: issue the slot atomic now so its
-    // round trip overlaps the quaternion update
-    if (p.cnt_next) insert_body(p.grid, p.cnt_next, p.ent_next, p.err, x.x, x.y, x.z, bi, i, kind);
+    Snap<T> sn;
+    sn.x = x.x; sn.y = x.y; sn.z = x.z; sn.r = bi;
+    p.snap_next[i] = sn;
+    // next step's broadphase: issue the slot atomic now so its round trip
+    // overlaps the quaternion update
+    if (p.next.cnt) insert_id(p.grid, p.next, p.err, x.x, x.y, x.z, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
     STAMP(5);
     const Q4<T> res = mj_mulquat(Q4<T>{T(0), w.x, w.y, w.z}, q);
     Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
@@ -438,9 +448,7 @@ template <typename T, int MAXP, int G>
 __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
-    __shared__ int32_t s_ent[MAXP * NB];
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
-    __shared__ int32_t t_ent[G > 1 ? MAXP * NB : 1];
     const int tid = threadIdx.x;
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
     STAMP(0);
@@ -455,19 +463,21 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     const int32_t i = p.lo + l;
 
     // ---- K1 first: the contact search reads only step-start data -----------
-    const V3<T> x = {p.st.px[l], p.st.py[l], p.st.pz[l]};
+    const Snap<T> self = p.snap_cur[i];
+    const V3<T> x = {self.x, self.y, self.z};
     const int32_t kind = p.cs.kind[i];
-    const T bi = p.cs.bound[i];
-    const V3<T> sz = {p.cs.sx[i], p.cs.sy[i], p.cs.sz[i]};
+    const T bi = self.r;
+    // half extents y, z only matter for boxes
+    const V3<T> sz = {p.cs.sx[i], kind != 0 ? p.cs.sy[i] : T(0), kind != 0 ? p.cs.sz[i] : T(0)};
     STAMP(1);
     int32_t np_ = 0;
     if (RB_ABLATE != 1) {
-        if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, s_ent, tid);
-        else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_ent, t_id, t_ent, slot, k, tid);
+        if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid);
+        else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, t_id, slot, k, tid);
     }
     STAMP(2);
     if (!active || k != 0) return;
-    body_update<T, MAXP, NB>(p, l, i, x, kind, sz, bi, np_, s_id, s_ent, slot, tid);
+    body_update<T, MAXP, NB>(p, l, i, x, kind, sz, bi, np_, s_id, slot, tid);
 }
 
 #if RB_STAMPS
@@ -564,8 +574,6 @@ template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, d
     return hipGetLastError();
 }
 
-template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
-template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_step<double>(const StepParams<double> &, int, bool, hipStream_t);
 template hipError_t launch_step<float>(const StepParams<float> &, int, bool, hipStream_t);
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
@@ -574,5 +582,7 @@ template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *
 template hipError_t launch_kat_impulse<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<float>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);
 
 }  // namespace rb

@@ -1,6 +1,8 @@
 """Body-range sharding of one scene over the GPUs of a node.
 
-Rank r owns bodies [r*S, r*S + S), S = ceil(N / P).  Each step is Jacobi
+Rank r owns bodies [r*S, r*S + S), S = ceil(N / P).  The exchange buffer
+holds (x, y, z, bounding radius) per body in global id order ([P][S][4]);
+two such buffers alternate step by step inside the library.  Each step is Jacobi
 across bodies (multi_sphere_bounce.py:43-46: one contact pass, then every
 body updated from step-start data), and the reference treats a contact
 partner as static (collision.py:27), so a rank needs only the step-start
@@ -38,6 +40,8 @@ class _DeviceBuffer:
 
 
 def wrap_gpos(world: World, torch):
+    """Torch view of the buffer the pending exchange fills (call between
+    shard_step and shard_exchange_done)."""
     ptr, shard_elems, esz = world.gpos_buffer()
     total = shard_elems * world.world_size
     t = torch.as_tensor(_DeviceBuffer(ptr, total, esz), device=f"cuda:{torch.cuda.current_device()}")
@@ -52,8 +56,9 @@ class ShardedWorld:
     gloo process groups, e.g. several ranks sharing one GPU in tests).
 
     `world_factory(rank, world_size)` may supply the per-rank stepper (any
-    object with the World shard interface and a `gpos_tensor(torch)`
-    method); by default it is a HIP World on `device`."""
+    object with the World shard interface and an `exchange_buffer(torch)`
+    method returning (tensor, shard_elems)); by default it is a HIP World on
+    `device`."""
 
     def __init__(self, scene: Scene, dtype: str = "f64", device: Optional[int] = None,
                  group=None, transport: Optional[str] = None, world_factory=None, **world_kw):
@@ -67,9 +72,9 @@ class ShardedWorld:
         else:
             self.rank, self.P, backend = 0, 1, None
         self.transport = transport or ("nccl" if backend == "nccl" else "host")
+        self._views = {}
         if world_factory is not None:
             self.world = world_factory(self.rank, self.P)
-            self.gpos, self.shard_elems = self.world.gpos_tensor(torch)
         else:
             if device is None:
                 device = torch.cuda.current_device()
@@ -78,18 +83,26 @@ class ShardedWorld:
                                **world_kw)
             self.stream = torch.cuda.current_stream(device)
             self.world.set_stream(self.stream.cuda_stream)
-            self.gpos, self.shard_elems = wrap_gpos(self.world, torch)
-        self.mine = self.gpos[self.rank * self.shard_elems:(self.rank + 1) * self.shard_elems]
+
+    def _buffer(self):
+        if hasattr(self.world, "exchange_buffer"):
+            return self.world.exchange_buffer(self.torch)
+        ptr = self.world.gpos_buffer()[0]
+        if ptr not in self._views:                 # two buffers alternate
+            self._views[ptr] = wrap_gpos(self.world, self.torch)
+        return self._views[ptr]
 
     def _exchange(self):
+        buf, n = self._buffer()
+        mine = buf[self.rank * n:(self.rank + 1) * n]
         if self.transport == "nccl":
             # in place: the input is this rank's chunk of the output buffer
-            self.dist.all_gather_into_tensor(self.gpos, self.mine, group=self.group)
+            self.dist.all_gather_into_tensor(buf, mine, group=self.group)
         else:
-            cpu = self.mine.to("cpu")
-            out = self.torch.empty(self.P * self.shard_elems, dtype=cpu.dtype)
+            cpu = mine.to("cpu")
+            out = self.torch.empty(self.P * n, dtype=cpu.dtype)
             self.dist.all_gather_into_tensor(out, cpu, group=self.group)
-            self.gpos.copy_(out.to(self.gpos.device))
+            buf.copy_(out.to(buf.device))
 
     def step(self, nsteps: int = 1, **params):
         if self.P == 1:
@@ -110,7 +123,7 @@ class ShardedWorld:
             return q, v
         t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
         if self.transport == "nccl":
-            t = t.to(self.gpos.device)
+            t = t.to(f"cuda:{self.torch.cuda.current_device()}")
         elif t.dtype != self.torch.float64:
             t = t.double()
         self.dist.all_reduce(t, group=self.group)      # rows are disjoint: sum == union

@@ -200,17 +200,17 @@ def test_shard_invariance_in_process(rb, P):
         ref.step(120)
         rq, rv = ref.get_state()
     worlds = [rb.World(sc, rank=r, world_size=P) for r in range(P)]
-    bufs = [wrap_gpos(w, torch) for w in worlds]
-    S3 = bufs[0][1]
     for _ in range(120):
         for w in worlds:
             w.shard_step()
         for w in worlds:
             w.sync()
+        bufs = [wrap_gpos(w, torch) for w in worlds]      # the buffers alternate per step
+        n = bufs[0][1]
         for r, (buf, _) in enumerate(bufs):
             for o, (obuf, _) in enumerate(bufs):
                 if o != r:
-                    buf[o * S3:(o + 1) * S3].copy_(obuf[o * S3:(o + 1) * S3])
+                    buf[o * n:(o + 1) * n].copy_(obuf[o * n:(o + 1) * n])
         torch.cuda.synchronize()
         for w in worlds:
             w.shard_exchange_done()

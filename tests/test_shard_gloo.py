@@ -34,7 +34,7 @@ class OracleShardStepper:
         for b in range(scene.n):
             g[b // self.S, :, b % self.S] = torch.from_numpy(self.q[b, 0:3])
 
-    def gpos_tensor(self, torch_mod):
+    def exchange_buffer(self, torch_mod):
         return self.buf, 3 * self.S
 
     def shard_step(self, **params):
