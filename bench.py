@@ -14,8 +14,10 @@ all-gather positions over RCCL every step.
 value = total bodies x K / (max over ranks of the timed region), with the
 state resident in HBM.  roofline: algorithmic HBM bytes of the step kernel
 (248 B per sphere body-step in fp64) x owned bodies / its
-average launch duration, measured with HIP events on the world's stream
-over a second run of K steps right after the timed region.
+average launch duration.  One rank: HIP events recorded on the world's
+stream (torch's current stream) around the timed region, which is exactly K
+graph-replayed step-kernel launches, / K.  Several ranks: an event pair
+around each step-kernel launch over a second run of K steps.
 cpu_baseline: the oracle (C restatement of the reference arithmetic, one
 core) on rank 0 at N=1 over the full C2 scene for 2,000 steps.
 """
