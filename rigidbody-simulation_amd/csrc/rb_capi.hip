@@ -83,15 +83,17 @@ struct rb_world {
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
-    int32_t *cnt[3] = {};      // [H] broadphase bucket counts
-    uint32_t *ids[3] = {};     // [H][BUCKET_SLOTS] broadphase bucket ids
+    int32_t *cnt[3] = {};      // [H] broadphase bucket counts (rotate mod 3)
+    uint32_t *ids[2] = {};     // [H][BUCKET_SLOTS] bucket slot ids (alternate with the snapshots)
+    void *pos[2] = {};         // [H][BUCKET_SLOTS] Snap<T> bucket slot snapshots
     int32_t *err = nullptr;
     int32_t *err_host = nullptr;   // pinned
     // recording
     bool record = false;
     int32_t *rec_count = nullptr, *rec_partner = nullptr, *rec_kind = nullptr;
     void *rec_dist = nullptr;
-    // stepping state: step counter c; tables rotate mod 3, snapshots mod 2
+    // stepping state: step counter c; bucket counts rotate mod 3, snapshots
+    // and bucket slots mod 2
     int64_t c = 0;
     bool primed = false;
     std::map<std::tuple<int64_t, int, double, double, double, double, int>, hipGraphExec_t> graphs;
@@ -117,7 +119,10 @@ template <typename T> Grid<T> make_grid(const rb_world *w) {
     return g;
 }
 
-Table table(const rb_world *w, int k) { return Table{w->cnt[k], w->ids[k]}; }
+// the broadphase of the step whose counts are cnt[ph] and slots [sp]
+template <typename T> Table<T> table(const rb_world *w, int ph, int sp) {
+    return Table<T>{w->cnt[ph], w->ids[sp], w->pos[sp] ? dp<Snap<T>>(w->pos[sp], 0) : nullptr};
+}
 
 // parameters of the step with counter value c
 template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt, double e, double mu, double thr,
@@ -146,8 +151,8 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     const int ph = (int)(c % 3), sp = (int)(c % 2);
     p.snap_cur = dp<Snap<T>>(w->snap[sp], 0);
     p.snap_next = dp<Snap<T>>(w->snap[1 - sp], 0);
-    p.cur = table(w, ph);
-    p.next = insert_next ? table(w, (ph + 1) % 3) : Table{nullptr, nullptr};
+    p.cur = table<T>(w, ph, sp);
+    p.next = insert_next ? table<T>(w, (ph + 1) % 3, 1 - sp) : Table<T>{nullptr, nullptr, nullptr};
     p.cnt_clear = w->cnt[(ph + 2) % 3];
     p.err = w->err;
     if (w->record) {
@@ -165,7 +170,7 @@ template <typename T> InsertParams<T> make_insert(rb_world *w, int sp, int ph, i
     ip.kind = w->kind;
     ip.first = first; ip.count = count; ip.skip_lo = skip_lo; ip.skip_hi = skip_hi;
     ip.grid = make_grid<T>(w);
-    ip.tab = table(w, ph);
+    ip.tab = table<T>(w, ph, sp);
     ip.err = w->err;
     return ip;
 }
@@ -366,7 +371,7 @@ void free_world(rb_world *w) {
     drop_graphs(w);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
-                    w->ids[0], w->ids[1], w->ids[2], w->err, w->rec_count, w->rec_partner, w->rec_kind,
+                    w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -448,9 +453,11 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     ALLOC(w->state, (size_t)w->esz * 10 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
-    for (int k = 0; k < 3; ++k) {
-        ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
+    for (int k = 0; k < 3; ++k) ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
+    for (int k = 0; k < 2; ++k) {
         ALLOC(w->ids[k], sizeof(uint32_t) * BUCKET_SLOTS * w->H);
+        // slot snapshots feed the cooperative (small-scene) search only
+        if (w->n_local <= w->coop_max) ALLOC(w->pos[k], (size_t)w->esz * 4 * BUCKET_SLOTS * w->H);
     }
     ALLOC(w->err, sizeof(int32_t));
 #undef ALLOC

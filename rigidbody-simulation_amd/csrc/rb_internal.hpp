@@ -23,14 +23,19 @@ enum : int32_t {
 // layout [P][S][4], rank r's bodies are the contiguous slice [r*S, r*S+S).
 template <typename T> struct alignas(4 * sizeof(T)) Snap { T x, y, z, r; };
 
-// Broadphase buckets: per-cell hash -> a count and a 128-byte line of body
-// ids.  A body claims its slot with one atomicAdd on the count; counts are
-// cleared two steps ahead by the step kernel's grid (ids are never cleared).
+// Broadphase buckets: per-cell hash -> a count, a 128-byte line of body ids
+// and, slot for slot, the bodies' snapshots, so a query reads candidates'
+// positions from the bucket it already holds instead of chasing ids into
+// the id-indexed snapshot.  A body claims its slot with one atomicAdd on the
+// count; counts are cleared two steps ahead by the step kernel's grid
+// (three count arrays rotate), slots are overwritten (two slot arrays
+// alternate with the snapshots).
 constexpr int BUCKET_SLOTS = 32;
 constexpr uint32_t BOX_FLAG = 0x80000000u;   // set on ids of box bodies
-struct Table {
+template <typename T> struct Table {
     int32_t *cnt;              // [H]
     uint32_t *ids;             // [H][BUCKET_SLOTS]
+    Snap<T> *pos;              // [H][BUCKET_SLOTS]; nullptr: not kept (one-lane search)
 };
 
 constexpr int MAX_PLANES = 8;
@@ -72,8 +77,8 @@ template <typename T> struct StepParams {
     Grid<T> grid;
     const Snap<T> *snap_cur;           // step-start snapshot (read)
     Snap<T> *snap_next;                // next step's snapshot (own rows written)
-    Table cur;                         // broadphase of snap_cur
-    Table next;                        // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
+    Table<T> cur;                      // broadphase of snap_cur
+    Table<T> next;                     // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
     int32_t *cnt_clear;                // counts of the table two steps ahead
     int32_t *err;
     // optional contact recording ([n_local][maxrec] slots)
@@ -88,7 +93,7 @@ template <typename T> struct InsertParams {
     int64_t first, count;              // global ids [first, first+count)
     int64_t skip_lo, skip_hi;          // global ids to skip (already inserted)
     Grid<T> grid;
-    Table tab;
+    Table<T> tab;
     int32_t *err;
 };
 

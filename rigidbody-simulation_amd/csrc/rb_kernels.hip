@@ -73,27 +73,43 @@ __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, in
     return true;
 }
 
-// Append an id to the bucket of (x, y, z): one returning atomicAdd claims
-// the slot.
+// Append a body (tagged id + snapshot) to the bucket of its cell: one
+// returning atomicAdd claims the slot (claim_slot), the slot is then
+// written (publish_slot).  Split so a caller can put independent work
+// between the two and hide the atomic's round trip.
+struct Claim { uint32_t b; int32_t slot; };      // slot < 0: not inserted
 template <typename T>
-__device__ __forceinline__ void insert_id(const Grid<T> &g, const Table &tab, int32_t *err, T x, T y, T z,
-                                          uint32_t tagged_id) {
+__device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn) {
     int32_t ix, iy, iz;
-    if (!cell_of(x, y, z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return; }
+    if (!cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return {0u, -1}; }
     const uint32_t b = bucket_of(ix, iy, iz, g.hmask);
-    const int32_t slot = atomicAdd(tab.cnt + b, 1);
-    if (slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    tab.ids[(int64_t)b * BUCKET_SLOTS + slot] = tagged_id;
+    return {b, atomicAdd(tab.cnt + b, 1)};
+}
+template <typename T>
+__device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
+                                             uint32_t tagged_id) {
+    if (c.slot < 0) return;
+    if (c.slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    const int64_t o = (int64_t)c.b * BUCKET_SLOTS + c.slot;
+    tab.ids[o] = tagged_id;
+    if (tab.pos) tab.pos[o] = sn;
+}
+template <typename T>
+__device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
+                                          uint32_t tagged_id) {
+    publish_slot(tab, err, claim_slot(g, tab, err, sn), sn, tagged_id);
 }
 
 // count (clamped) and the first 4 ids of a bucket, loaded together
-__device__ __forceinline__ uint4 bucket_head(const Table &tab, uint32_t b, int32_t &count) {
+template <typename T>
+__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int32_t &count) {
     const int32_t c = tab.cnt[b];
     const uint4 h = *reinterpret_cast<const uint4 *>(tab.ids + (int64_t)b * BUCKET_SLOTS);
     count = c < BUCKET_SLOTS ? c : BUCKET_SLOTS;
     return h;
 }
-__device__ __forceinline__ uint32_t bucket_id(const Table &tab, uint32_t b, const uint4 &h, int s) {
+template <typename T>
+__device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s) {
     return s == 0 ? h.x : s == 1 ? h.y : s == 2 ? h.z : s == 3 ? h.w : tab.ids[(int64_t)b * BUCKET_SLOTS + s];
 }
 
@@ -103,8 +119,7 @@ __global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
     if (k >= p.count) return;
     const int64_t id = p.first + k;
     if (id >= p.skip_lo && id < p.skip_hi) return;
-    const Snap<T> s = p.snap[id];
-    insert_id(p.grid, p.tab, p.err, s.x, s.y, s.z, (uint32_t)id | (p.kind[id] != 0 ? BOX_FLAG : 0u));
+    insert_id(p.grid, p.tab, p.err, p.snap[id], (uint32_t)id | (p.kind[id] != 0 ? BOX_FLAG : 0u));
 }
 
 template <typename T>
@@ -252,6 +267,8 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
             if (base + u < total && addr >= 0) t = p.cur.ids[addr];
             tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
+        // the id-indexed snapshot: ids are spatially coherent, so a wave's
+        // candidates share lines (cheaper than bucket slots at this scale)
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[tj[u] & ~BOX_FLAG];
 #pragma unroll
@@ -264,16 +281,20 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
-// cell k (its count, ids and candidate snapshots are fetched in parallel
-// with the other cells').  Hits become a bitmask over the bucket slots; a
-// group prefix sum (shuffles) places them in LDS and the group rank-sorts
-// them by body id.  Same contact set and order as search_partners.
+// cell k.  Its count, first ids and first RB_QBATCH slot snapshots are
+// loaded together (slots past the count are stale and ignored), and while
+// they are in flight the lane evaluates the body's inverse world inertia
+// (pre).  Hits become a bitmask over the bucket slots; a group prefix sum
+// (shuffles) places them — id and snapshot — in LDS, and the group
+// rank-sorts them by body id into s_id / s_pos.  Same contact set and order
+// as search_partners.
 template <typename T, int MAXP, int G>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
-                                               V3<T> x, T rad, T bi, int32_t *s_id, int32_t *t_id, int slot, int k,
-                                               int lane) {
+                                               V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
+                                               Snap<T> *t_pos, int slot, int k, int lane, LazyInvI<T> &pre) {
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
+    constexpr int QB = RB_QBATCH;
     int32_t cx = 0, cy = 0, cz = 0, sx = 1, sy = 1, sz = 1;
     bool ok = active;
     if (active && !neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) {
@@ -282,9 +303,16 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     }
     const uint32_t b = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0),
                                  p.grid.hmask);
+    const int64_t base = (int64_t)b * BUCKET_SLOTS;
     int32_t c = 0;
     uint4 id4 = {0, 0, 0, 0};
-    if (ok) id4 = bucket_head(p.cur, b, c);
+    Snap<T> p4[QB];
+    if (ok) {
+        id4 = bucket_head(p.cur, b, c);
+#pragma unroll
+        for (int u = 0; u < QB; ++u) p4[u] = p.cur.pos[base + u];
+    }
+    pre.get();                                    // overlaps the bucket loads
     const int gbase = lane & ~(G - 1);
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -292,38 +320,45 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         if (j < k && bj == b) c = 0;                  // bucket already visited by a lower cell
     }
     uint32_t mask = 0;
-    for (int s0 = 0; s0 < c; s0 += RB_QBATCH) {
-        uint32_t tj[RB_QBATCH];
-        Snap<T> sn[RB_QBATCH];
 #pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) {
-            const int s = s0 + u;
-            uint32_t t = (uint32_t)i;
-            if (s < c) t = bucket_id(p.cur, b, id4, s);
-            tj[u] = t;
+    for (int u = 0; u < QB; ++u)
+        if (u < c && candidate_hit(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u])) mask |= 1u << u;
+    for (int s0 = QB; s0 < c; s0 += QB) {
+        uint32_t tj[QB];
+        Snap<T> sn[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+            tj[u] = p.cur.ids[base + s0 + u];
+            sn[u] = p.cur.pos[base + s0 + u];
         }
 #pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[tj[u] & ~BOX_FLAG];
-#pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u)
-            if (candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
+        for (int u = 0; u < QB; ++u)
+            if (s0 + u < c && candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
     }
     const int h = __popc(mask);
-    int pre = 0, total = 0;
+    int pre_n = 0, total = 0;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
         const int hj = __shfl(h, gbase + j);
         total += hj;
-        if (j < k) pre += hj;
+        if (j < k) pre_n += hj;
     }
     if (total > MAXP && k == 0) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
-    int o = pre;
-    while (mask) {
-        const int sl = __builtin_ctz(mask);
-        mask &= mask - 1;
+    int o = pre_n;
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+        if (!((mask >> u) & 1u)) continue;
         if (o < MAXP) {
-            const uint32_t t = bucket_id(p.cur, b, id4, sl);
-            t_id[slot * MAXP + o] = (int32_t)t;
+            t_id[slot * MAXP + o] = (int32_t)bucket_id(p.cur, b, id4, u);
+            t_pos[slot * MAXP + o] = p4[u];
+        }
+        ++o;
+    }
+    for (uint32_t rest = mask & ~((1u << QB) - 1u); rest; rest &= rest - 1) {
+        const int sl = __builtin_ctz(rest);
+        if (o < MAXP) {                               // re-read: L1-hot from the batch above
+            t_id[slot * MAXP + o] = (int32_t)p.cur.ids[base + sl];
+            t_pos[slot * MAXP + o] = p.cur.pos[base + sl];
         }
         ++o;
     }
@@ -334,24 +369,43 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         int r = 0;
         for (int j = 0; j < tot; ++j) r += t_id[slot * MAXP + j] < id;
         s_id[r * NB + slot] = id;
+        s_pos[r * NB + slot] = t_pos[slot * MAXP + qq];
     }
     __syncthreads();
     return tot;
 }
 
+// Per-body inputs of K2, loaded by the cooperative form before the search
+// (their latency hides under it) and by the one-lane form after it (fewer
+// registers live across the search).
+template <typename T> struct BodyIn {
+    Q4<T> q;
+    V3<T> v, w;
+    T m;
+    V3<T> I;
+};
+template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepParams<T> &p, int32_t l, int32_t i) {
+    BodyIn<T> b;
+    b.q = {p.st.qw[l], p.st.qx[l], p.st.qy[l], p.st.qz[l]};
+    b.v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
+    b.w = {p.st.wx[l], p.st.wy[l], p.st.wz[l]};
+    b.m = p.cs.mass[i];
+    b.I = {p.cs.ix[i], p.cs.iy[i], p.cs.iz[i]};
+    return b;
+}
+
 // Everything after the contact search for one body (lane): gravity, the
 // Gauss-Seidel solves in canonical order, integration, next-step insert.
+// s_pos: the partners' snapshots in LDS (cooperative form), or nullptr to
+// read them from the step-start snapshot.
 template <typename T, int MAXP, int NB>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
-                                            V3<T> sz, T bi, int32_t np_, const int32_t *s_id, int slot, int tid) {
-    // ---- state (coalesced SoA) ----------------------------------------------
-    const Q4<T> q = {p.st.qw[l], p.st.qx[l], p.st.qy[l], p.st.qz[l]};
-    V3<T> v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
-    V3<T> w = {p.st.wx[l], p.st.wy[l], p.st.wz[l]};
-    const T m = p.cs.mass[i];
-    LazyInvI<T> invI;
-    invI.I = {p.cs.ix[i], p.cs.iy[i], p.cs.iz[i]};
-    invI.q = q;
+                                            V3<T> sz, T bi, const BodyIn<T> &in, LazyInvI<T> &invI, int32_t np_,
+                                            const int32_t *s_id, const Snap<T> *s_pos, int slot, int tid) {
+    const Q4<T> q = in.q;
+    V3<T> v = in.v;
+    V3<T> w = in.w;
+    const T m = in.m;
 
     // ---- a4: gravity / applied force (collision.py:66-70) ------------------
     {
@@ -395,13 +449,13 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     }
 
     // ---- K2: sphere partners in ascending id order ---------------------------
-    // (partner snapshots re-read 4 at a time — L1/L2-hot from the search;
-    // the solve itself is the reference's sequential Gauss-Seidel)
+    // (partner snapshots from LDS, or re-read 4 at a time; the solve itself
+    // is the reference's sequential Gauss-Seidel)
     for (int s0 = 0; s0 < np_; s0 += 4) {
         Snap<T> pe[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (s0 + u < np_) pe[u] = p.snap_cur[s_id[(s0 + u) * NB + slot]];
+            if (s0 + u < np_) pe[u] = s_pos ? s_pos[(s0 + u) * NB + slot] : p.snap_cur[s_id[(s0 + u) * NB + slot]];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (s0 + u >= np_) break;
@@ -428,37 +482,30 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     x = {x.x + v.x * p.dt, x.y + v.y * p.dt, x.z + v.z * p.dt};
     Snap<T> sn;
     sn.x = x.x; sn.y = x.y; sn.z = x.z; sn.r = bi;
+    // next step's broadphase: the slot atomic goes first (a later load or
+    // atomic would wait for every older store), its round trip overlaps the
+    // snapshot store and the quaternion update
+    Claim cl{0u, -1};
+    if (p.next.cnt) cl = claim_slot(p.grid, p.next, p.err, sn);
     p.snap_next[i] = sn;
-    // next step's broadphase: issue the slot atomic now so its round trip
-    // overlaps the quaternion update
-    if (p.next.cnt) insert_id(p.grid, p.next, p.err, x.x, x.y, x.z, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
     STAMP(5);
     const Q4<T> res = mj_mulquat(Q4<T>{T(0), w.x, w.y, w.z}, q);
     Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
                 q.y + (T(0.5) * res.y) * p.dt, q.z + (T(0.5) * res.z) * p.dt};
     const T nq = sqroot(fmadd(qn.z, qn.z, fmadd(qn.y, qn.y, fmadd(qn.x, qn.x, qn.w * qn.w))));
     qn = {qn.w / nq, qn.x / nq, qn.y / nq, qn.z / nq};
-    p.st.qw[l] = qn.w; p.st.qx[l] = qn.x; p.st.qy[l] = qn.y; p.st.qz[l] = qn.z;
     p.st.vx[l] = v.x; p.st.vy[l] = v.y; p.st.vz[l] = v.z;
     p.st.wx[l] = w.x; p.st.wy[l] = w.y; p.st.wz[l] = w.z;
+    p.st.qw[l] = qn.w; p.st.qx[l] = qn.x; p.st.qy[l] = qn.y; p.st.qz[l] = qn.z;
+    publish_slot(p.next, p.err, cl, sn, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
     STAMP(6);
 }
 
+// One body (G lanes): contact search, then (lane 0) the update.
 template <typename T, int MAXP, int G>
-__global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
-    constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
-    __shared__ int32_t s_id[MAXP * NB];
-    __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
-    const int tid = threadIdx.x;
-    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
-    STAMP(0);
-
-    // the table of step t+2 was last read by step t-1: clear it for t+1's inserts
-    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
-    const int slot = tid / G, k = tid % G;
-    const int64_t lb = (int64_t)blockIdx.x * NB + slot;
-    const bool active = lb < p.n_local;
-    if (G == 1 && !active) return;
+__device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
+                                          int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos) {
+    constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = p.lo + l;
 
@@ -469,15 +516,51 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     const T bi = self.r;
     // half extents y, z only matter for boxes
     const V3<T> sz = {p.cs.sx[i], kind != 0 ? p.cs.sy[i] : T(0), kind != 0 ? p.cs.sz[i] : T(0)};
+    BodyIn<T> in;
+    LazyInvI<T> invI;
+    if constexpr (G > 1) {
+        in = load_body(p, l, i);
+        invI.I = in.I;
+        invI.q = in.q;
+    }
     STAMP(1);
     int32_t np_ = 0;
-    if (RB_ABLATE != 1) {
-        if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid);
-        else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, t_id, slot, k, tid);
+    if constexpr (G == 1) {
+        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid);
+    } else {
+        if (RB_ABLATE != 1)
+            np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
+                                          invI);
     }
     STAMP(2);
     if (!active || k != 0) return;
-    body_update<T, MAXP, NB>(p, l, i, x, kind, sz, bi, np_, s_id, slot, tid);
+    if constexpr (G == 1) {
+        in = load_body(p, l, i);
+        invI.I = in.I;
+        invI.q = in.q;
+    }
+    body_update<T, MAXP, NB>(p, l, i, x, kind, sz, bi, in, invI, np_, s_id, G > 1 ? s_pos : nullptr, slot, tid);
+}
+
+template <typename T, int MAXP, int G>
+__global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
+    constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
+    __shared__ int32_t s_id[MAXP * NB];
+    __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
+    __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
+    __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
+    const int tid = threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
+    STAMP(0);
+
+    const int slot = tid / G, k = tid % G;
+    const int64_t lb = (int64_t)blockIdx.x * NB + slot;
+    const bool active = lb < p.n_local;
+    if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos);
+    // The counts of step t+2's table were last read by step t-1: clear them
+    // for step t+1's inserts.  Last, since every load or atomic issued after
+    // a store waits for it (vmcnt counts in issue order).
+    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
 }
 
 #if RB_STAMPS
