@@ -86,6 +86,8 @@ struct rb_world {
     int32_t *cnt[3] = {};      // [H] broadphase bucket counts (rotate mod 3)
     uint32_t *ids[2] = {};     // [H][BUCKET_SLOTS] bucket slot ids (alternate with the snapshots)
     void *pos[2] = {};         // [H][BUCKET_SLOTS] Snap<T> bucket slot snapshots
+    int32_t *plist = nullptr;      // split form: [MAXP][S] sorted partner ids
+    int32_t *plist_cnt = nullptr;  // split form: [S] partner counts
     int32_t *err = nullptr;
     int32_t *err_host = nullptr;   // pinned
     // recording
@@ -155,6 +157,8 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.next = insert_next ? table<T>(w, (ph + 1) % 3, 1 - sp) : Table<T>{nullptr, nullptr, nullptr};
     p.cnt_clear = w->cnt[(ph + 2) % 3];
     p.err = w->err;
+    p.plist = w->plist;
+    p.plist_cnt = w->plist_cnt;
     if (w->record) {
         p.rec_count = w->rec_count; p.rec_partner = w->rec_partner; p.rec_kind = w->rec_kind;
         p.rec_dist = dp<T>(w->rec_dist, 0);
@@ -371,7 +375,7 @@ void free_world(rb_world *w) {
     drop_graphs(w);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
-                    w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
+                    w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -454,10 +458,20 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
     for (int k = 0; k < 3; ++k) ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
+    // Experimental, opt-in (RBHIP_SPLIT=1): large scenes step in two kernels
+    // (search, update) joined by a partner list.  Not yet validated on the
+    // device; the default is the fused one-kernel step.
+    const char *split_env = getenv("RBHIP_SPLIT");
+    const bool coop = w->n_local <= w->coop_max;
+    const bool split = !coop && split_env && atoi(split_env) == 1;
+    if (split) {
+        ALLOC(w->plist, sizeof(int32_t) * (w->maxp <= 16 ? 16 : 32) * w->S);
+        ALLOC(w->plist_cnt, sizeof(int32_t) * w->S);
+    }
     for (int k = 0; k < 2; ++k) {
         ALLOC(w->ids[k], sizeof(uint32_t) * BUCKET_SLOTS * w->H);
-        // slot snapshots feed the cooperative (small-scene) search only
-        if (w->n_local <= w->coop_max) ALLOC(w->pos[k], (size_t)w->esz * 4 * BUCKET_SLOTS * w->H);
+        // slot snapshots feed the cooperative search only
+        if (needs_slot_snapshots(coop, split)) ALLOC(w->pos[k], (size_t)w->esz * 4 * BUCKET_SLOTS * w->H);
     }
     ALLOC(w->err, sizeof(int32_t));
 #undef ALLOC

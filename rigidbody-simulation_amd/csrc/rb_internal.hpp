@@ -81,6 +81,8 @@ template <typename T> struct StepParams {
     Table<T> next;                     // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
     int32_t *cnt_clear;                // counts of the table two steps ahead
     int32_t *err;
+    // split form only: sorted partner ids [MAXP][S] and counts [S]
+    int32_t *plist, *plist_cnt;
     // optional contact recording ([n_local][maxrec] slots)
     int32_t *rec_count, *rec_partner, *rec_kind;
     T *rec_dist;
@@ -105,5 +107,15 @@ template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in,
 template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s);
 
 constexpr int STEP_BLOCK = 64;
+
+// lanes per body of the split form's search kernel (1, or 8 = the
+// cooperative search, which reads the bucket slot snapshots)
+#ifndef RB_SPLIT_G
+#define RB_SPLIT_G 1
+#endif
+constexpr int SPLIT_SEARCH_LANES = RB_SPLIT_G;
+
+// does a world stepping with these forms need bucket slot snapshots?
+inline bool needs_slot_snapshots(bool coop, bool split) { return coop || (split && SPLIT_SEARCH_LANES > 1); }
 
 }  // namespace rb

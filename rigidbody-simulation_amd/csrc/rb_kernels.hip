@@ -24,7 +24,8 @@
 #include "rb_internal.hpp"
 
 // diagnostic builds only (scripts/ablate.py): 1 = skip the sphere-sphere
-// broadphase, 2 = skip the world-inertia inverse (identity), 0 = product
+// broadphase, 2 = skip the world-inertia inverse (identity), 3 = empty
+// kernel (launch floor), 4 = search only (no body update), 0 = product
 #ifndef RB_ABLATE
 #define RB_ABLATE 0
 #endif
@@ -33,7 +34,7 @@
 #define RB_STAMPS 0
 #endif
 #if RB_STAMPS
-__device__ unsigned long long rb_stamp_buf[1 << 16][8];
+__device__ unsigned long long rb_stamp_buf[1 << 16][16];
 #define STAMP(k)                                                                                  \
     do {                                                                                          \
         __builtin_amdgcn_sched_barrier(0);                                                        \
@@ -50,7 +51,61 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][8];
 #define RB_QBATCH 4
 #endif
 
+// write-through (sc1) stores for everything the next step reads: the lines
+// leave L2 as they are written, so the end-of-kernel L2 writeback has
+// nothing left to flush
+#ifndef RB_WT
+#define RB_WT 0
+#endif
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
+// so block b runs body-block xcd_block(b) and each XCD (own L2) steps one
+// contiguous id range = one spatial region of the scene
+#ifndef RB_XCD_REMAP
+#define RB_XCD_REMAP 1
+#endif
+
 namespace rb {
+
+// diagnostic build only (RB_BOUNDS=1): index checks that report and clamp
+// instead of faulting
+#ifndef RB_BOUNDS
+#define RB_BOUNDS 0
+#endif
+__device__ __forceinline__ int64_t chk(int64_t idx, int64_t n, int line) {
+#if RB_BOUNDS
+    if (idx < 0 || idx >= n) {
+        printf("RB_BOUNDS line %d: index %lld outside [0, %lld) block %d thread %d\n", line, (long long)idx,
+               (long long)n, (int)blockIdx.x, (int)threadIdx.x);
+        return 0;
+    }
+#else
+    (void)n; (void)line;
+#endif
+    return idx;
+}
+#define CHK(idx, n) chk((idx), (n), __LINE__)
+
+constexpr uint32_t N_XCD = 8;
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+#if RB_XCD_REMAP
+    const uint32_t q = nb / N_XCD, r = nb % N_XCD, x = b % N_XCD;
+    return x * q + (x < r ? x : r) + b / N_XCD;
+#else
+    (void)nb;
+    return b;
+#endif
+}
+
+template <typename V> __device__ __forceinline__ void wt_store(V *ptr, V v) {
+#if RB_WT
+    __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *ptr = v;
+#endif
+}
+template <typename T> __device__ __forceinline__ void wt_store(Snap<T> *ptr, const Snap<T> &v) {
+    wt_store(&ptr->x, v.x); wt_store(&ptr->y, v.y); wt_store(&ptr->z, v.z); wt_store(&ptr->r, v.r);
+}
 
 // cell -> bucket: murmur3-finalised hash of the cell coordinates
 __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, uint32_t hmask) {
@@ -90,9 +145,9 @@ __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, 
                                              uint32_t tagged_id) {
     if (c.slot < 0) return;
     if (c.slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    const int64_t o = (int64_t)c.b * BUCKET_SLOTS + c.slot;
-    tab.ids[o] = tagged_id;
-    if (tab.pos) tab.pos[o] = sn;
+    const int64_t o = CHK((int64_t)c.b * BUCKET_SLOTS + c.slot, RB_BOUNDS ? 1ll << 40 : 0);
+    wt_store(tab.ids + o, tagged_id);
+    if (tab.pos) wt_store(tab.pos + o, sn);
 }
 template <typename T>
 __device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
@@ -103,7 +158,7 @@ __device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab,
 // count (clamped) and the first 4 ids of a bucket, loaded together
 template <typename T>
 __device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int32_t &count) {
-    const int32_t c = tab.cnt[b];
+    const int32_t c = tab.cnt[CHK(b, RB_BOUNDS ? 1ll << 40 : 0)];
     const uint4 h = *reinterpret_cast<const uint4 *>(tab.ids + (int64_t)b * BUCKET_SLOTS);
     count = c < BUCKET_SLOTS ? c : BUCKET_SLOTS;
     return h;
@@ -232,7 +287,7 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
     for (int k = 0; k < 8; ++k)
         b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid.hmask);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) id4[k] = bucket_head(p.cur, b[k], c[k]);
+    for (int k = 0; k < 8; ++k) id4[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H), c[k]);
     int32_t total = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -264,13 +319,13 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
                 }
                 rem -= c[k];
             }
-            if (base + u < total && addr >= 0) t = p.cur.ids[addr];
+            if (base + u < total && addr >= 0) t = p.cur.ids[CHK(addr, (int64_t)p.grid.H * BUCKET_SLOTS)];
             tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
         // the id-indexed snapshot: ids are spatially coherent, so a wave's
         // candidates share lines (cheaper than bucket slots at this scale)
 #pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[tj[u] & ~BOX_FLAG];
+        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u)
             if (candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u]))
@@ -284,14 +339,14 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
 // cell k.  Its count, first ids and first RB_QBATCH slot snapshots are
 // loaded together (slots past the count are stale and ignored), and while
 // they are in flight the lane evaluates the body's inverse world inertia
-// (pre).  Hits become a bitmask over the bucket slots; a group prefix sum
+// (pre, optional).  Hits become a bitmask over the bucket slots; a group prefix sum
 // (shuffles) places them — id and snapshot — in LDS, and the group
 // rank-sorts them by body id into s_id / s_pos.  Same contact set and order
 // as search_partners.
 template <typename T, int MAXP, int G>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
                                                V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
-                                               Snap<T> *t_pos, int slot, int k, int lane, LazyInvI<T> &pre) {
+                                               Snap<T> *t_pos, int slot, int k, int lane, LazyInvI<T> *pre) {
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
     constexpr int QB = RB_QBATCH;
@@ -304,6 +359,8 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     const uint32_t b = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0),
                                  p.grid.hmask);
     const int64_t base = (int64_t)b * BUCKET_SLOTS;
+    [[maybe_unused]] const int tid = lane;   // STAMP
+    STAMP(8);
     int32_t c = 0;
     uint4 id4 = {0, 0, 0, 0};
     Snap<T> p4[QB];
@@ -312,7 +369,8 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
 #pragma unroll
         for (int u = 0; u < QB; ++u) p4[u] = p.cur.pos[base + u];
     }
-    pre.get();                                    // overlaps the bucket loads
+    if (pre) pre->get();                          // overlaps the bucket loads
+    STAMP(9);
     const int gbase = lane & ~(G - 1);
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -335,6 +393,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         for (int u = 0; u < QB; ++u)
             if (s0 + u < c && candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
     }
+    STAMP(10);
     const int h = __popc(mask);
     int pre_n = 0, total = 0;
 #pragma unroll
@@ -363,6 +422,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         ++o;
     }
     __syncthreads();
+    STAMP(11);
     const int tot = total < MAXP ? total : MAXP;
     for (int qq = k; qq < tot; qq += G) {
         const int32_t id = t_id[slot * MAXP + qq];
@@ -394,14 +454,22 @@ template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepP
     return b;
 }
 
+// Where body_update finds a body's sorted partner list: ids at id[u *
+// stride] (an LDS column, or the global per-slot list of the split form),
+// snapshots at pos[u * stride] (LDS, cooperative form) or, pos == nullptr,
+// gathered from the step-start snapshot.
+template <typename T> struct Partners {
+    const int32_t *id;
+    int64_t stride;
+    const Snap<T> *pos;
+};
+
 // Everything after the contact search for one body (lane): gravity, the
 // Gauss-Seidel solves in canonical order, integration, next-step insert.
-// s_pos: the partners' snapshots in LDS (cooperative form), or nullptr to
-// read them from the step-start snapshot.
-template <typename T, int MAXP, int NB>
+template <typename T>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, LazyInvI<T> &invI, int32_t np_,
-                                            const int32_t *s_id, const Snap<T> *s_pos, int slot, int tid) {
+                                            const Partners<T> &P, int tid) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -449,17 +517,21 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     }
 
     // ---- K2: sphere partners in ascending id order ---------------------------
-    // (partner snapshots from LDS, or re-read 4 at a time; the solve itself
-    // is the reference's sequential Gauss-Seidel)
+    // (partner snapshots fetched 4 at a time; the solve itself is the
+    // reference's sequential Gauss-Seidel)
     for (int s0 = 0; s0 < np_; s0 += 4) {
+        int32_t jj[4];
         Snap<T> pe[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (s0 + u < np_) pe[u] = s_pos ? s_pos[(s0 + u) * NB + slot] : p.snap_cur[s_id[(s0 + u) * NB + slot]];
+            if (s0 + u < np_) jj[u] = P.id[CHK((s0 + u) * P.stride, 32 * P.stride)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (s0 + u < np_) pe[u] = P.pos ? P.pos[(s0 + u) * P.stride] : p.snap_cur[CHK(jj[u], p.n_global)];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (s0 + u >= np_) break;
-            const int32_t j = s_id[(s0 + u) * NB + slot];
+            const int32_t j = jj[u];
             const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};
             const T rj = pe[u].r;
             Contact<T> con;
@@ -487,16 +559,17 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // snapshot store and the quaternion update
     Claim cl{0u, -1};
     if (p.next.cnt) cl = claim_slot(p.grid, p.next, p.err, sn);
-    p.snap_next[i] = sn;
+    wt_store(p.snap_next + i, sn);
     STAMP(5);
     const Q4<T> res = mj_mulquat(Q4<T>{T(0), w.x, w.y, w.z}, q);
     Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
                 q.y + (T(0.5) * res.y) * p.dt, q.z + (T(0.5) * res.z) * p.dt};
     const T nq = sqroot(fmadd(qn.z, qn.z, fmadd(qn.y, qn.y, fmadd(qn.x, qn.x, qn.w * qn.w))));
     qn = {qn.w / nq, qn.x / nq, qn.y / nq, qn.z / nq};
-    p.st.vx[l] = v.x; p.st.vy[l] = v.y; p.st.vz[l] = v.z;
-    p.st.wx[l] = w.x; p.st.wy[l] = w.y; p.st.wz[l] = w.z;
-    p.st.qw[l] = qn.w; p.st.qx[l] = qn.x; p.st.qy[l] = qn.y; p.st.qz[l] = qn.z;
+    wt_store(p.st.vx + l, v.x); wt_store(p.st.vy + l, v.y); wt_store(p.st.vz + l, v.z);
+    wt_store(p.st.wx + l, w.x); wt_store(p.st.wy + l, w.y); wt_store(p.st.wz + l, w.z);
+    wt_store(p.st.qw + l, qn.w); wt_store(p.st.qx + l, qn.x); wt_store(p.st.qy + l, qn.y);
+    wt_store(p.st.qz + l, qn.z);
     publish_slot(p.next, p.err, cl, sn, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
     STAMP(6);
 }
@@ -530,16 +603,17 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     } else {
         if (RB_ABLATE != 1)
             np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                          invI);
+                                          &invI);
     }
     STAMP(2);
-    if (!active || k != 0) return;
+    if (!active || k != 0 || RB_ABLATE == 4) return;
     if constexpr (G == 1) {
         in = load_body(p, l, i);
         invI.I = in.I;
         invI.q = in.q;
     }
-    body_update<T, MAXP, NB>(p, l, i, x, kind, sz, bi, in, invI, np_, s_id, G > 1 ? s_pos : nullptr, slot, tid);
+    const Partners<T> P{s_id + slot, NB, G > 1 ? s_pos + slot : nullptr};
+    body_update<T>(p, l, i, x, kind, sz, bi, in, invI, np_, P, tid);
 }
 
 template <typename T, int MAXP, int G>
@@ -551,21 +625,78 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
     const int tid = threadIdx.x;
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
+    if (RB_ABLATE == 3) return;
     STAMP(0);
 
     const int slot = tid / G, k = tid % G;
-    const int64_t lb = (int64_t)blockIdx.x * NB + slot;
+    const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < p.n_local;
     if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos);
     // The counts of step t+2's table were last read by step t-1: clear them
     // for step t+1's inserts.  Last, since every load or atomic issued after
     // a store waits for it (vmcnt counts in issue order).
-    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) p.cnt_clear[h] = 0;
+    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
+}
+
+// ---- split form (large scenes): search kernel + update kernel -------------
+// The fused kernel's register footprint (the f64 solve) caps it at two
+// waves per SIMD, too few to hide the search's dependent random loads.
+// Split, the search runs at high occupancy and hands each body's sorted
+// partner ids to the update through a per-slot list in HBM ([MAXP][S],
+// coalesced by slot).
+template <typename T, int MAXP, int G>
+__global__ __launch_bounds__(STEP_BLOCK) void search_kernel(StepParams<T> p) {
+    constexpr int NB = STEP_BLOCK / G;
+    __shared__ int32_t s_id[MAXP * NB];
+    __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
+    __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
+    __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
+    const int tid = threadIdx.x;
+    const int slot = tid / G, k = tid % G;
+    const int64_t lb = (int64_t)blockIdx.x * NB + slot;
+    const bool active = lb < p.n_local;
+    if (G == 1 && !active) return;
+    const int32_t l = active ? (int32_t)lb : 0;
+    const int32_t i = p.lo + l;
+    const Snap<T> self = p.snap_cur[CHK(i, p.n_global)];
+    const V3<T> x = {self.x, self.y, self.z};
+    const int32_t kind = p.cs.kind[i];
+    const T rad = p.cs.sx[i];
+    int32_t np_;
+    if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, rad, self.r, s_id, tid);
+    else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
+                                       (LazyInvI<T> *)nullptr);
+    if (!active) return;
+    for (int s = k; s < np_; s += G) p.plist[CHK((int64_t)s * p.S + l, (int64_t)MAXP * p.S)] = s_id[s * NB + slot];
+    if (k == 0) p.plist_cnt[CHK(l, p.S)] = np_;
+}
+
+template <typename T>
+__global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
+    const int tid = threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
+    const int64_t lb = gt;
+    if (lb < p.n_local) {
+        const int32_t l = (int32_t)lb, i = p.lo + l;
+        const Snap<T> self = p.snap_cur[CHK(i, p.n_global)];
+        const V3<T> x = {self.x, self.y, self.z};
+        const int32_t kind = p.cs.kind[i];
+        const V3<T> sz = {p.cs.sx[i], kind != 0 ? p.cs.sy[i] : T(0), kind != 0 ? p.cs.sz[i] : T(0)};
+        const BodyIn<T> in = load_body(p, l, i);
+        LazyInvI<T> invI;
+        invI.I = in.I;
+        invI.q = in.q;
+        const int32_t np_ = p.plist_cnt[CHK(l, p.S)];
+        if (RB_BOUNDS && np_ > 16) printf("RB_BOUNDS np_ %d at l %d\n", np_, l);
+        const Partners<T> P{p.plist + l, p.S, nullptr};
+        body_update<T>(p, l, i, x, kind, sz, self.r, in, invI, np_, P, tid);
+    }
+    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
 }
 
 #if RB_STAMPS
 extern "C" int rb_diag_stamps(unsigned long long *out, int nblocks) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 8 * nblocks);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 16 * nblocks);
 }
 #endif
 
@@ -622,7 +753,17 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, b
     const int nb = coop ? STEP_BLOCK / 8 : STEP_BLOCK;
     int64_t blocks = (p.n_local + nb - 1) / nb;
     if (blocks < 1) blocks = 1;
-    if (coop) {
+    const bool split = !coop && p.plist;
+    // the cooperative search reads bucket slot snapshots: never launch it
+    // on a table without them
+    if (needs_slot_snapshots(coop, split) && (!p.cur.pos || (p.next.cnt && !p.next.pos))) return hipErrorInvalidValue;
+    if (split) {
+        constexpr int GS = SPLIT_SEARCH_LANES;
+        const int64_t sblocks = blocks * GS;
+        if (maxp <= 16) hipLaunchKernelGGL((search_kernel<T, 16, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
+        hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    } else if (coop) {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16, 8>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel<T, 32, 8>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     } else {

@@ -1,4 +1,4 @@
-"""Diagnostic: time the step kernel (HIP events per launch) for several
+"""Diagnostic: time the step kernel (graph replay, or GRAPH=0: HIP events per launch) for several
 builds (VARIANTS: ";"-separated extra compiler flags) and runtime settings
 (ENVS: ";"-separated NAME=VALUE applied before each world is created), over
 several flat-sphere scene sizes, interleaved in one process.  Not part of the
@@ -16,6 +16,8 @@ for k, v in enumerate(variants):
     subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
                    f"{v} -o {out} rb_kernels.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
     paths[v] = out
+import torch  # noqa: E402  (initialise torch's HIP context before the library's)
+torch.cuda.init()
 from rbhip import _lib, scenes
 import rbhip.world as W
 res = {}
@@ -30,10 +32,20 @@ for rnd in range(2):
             for nx, ny in sizes:
                 sc = scenes.flat_spheres(nx, ny, seed=0)
                 with W.World(sc) as w:
-                    w.step(60)
-                    w.kernel_timing(True)
-                    w.step(100)
-                    avg, n = w.kernel_timing(False)
+                    if os.environ.get("GRAPH", "1") == "1":
+                        # K graph-replayed steps between HIP events on torch's stream
+                        w.set_stream(torch.cuda.current_stream().cuda_stream)
+                        w.step(60)
+                        w.step(200)
+                        torch.cuda.synchronize()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(); w.step(200); e1.record(); torch.cuda.synchronize()
+                        avg = e0.elapsed_time(e1) / 200
+                    else:
+                        w.step(60)
+                        w.kernel_timing(True)
+                        w.step(100)
+                        avg, n = w.kernel_timing(False)
                 res.setdefault((v, env, nx * ny), []).append(avg)
             if env:
                 del os.environ[env.split("=")[0]]
