@@ -18,8 +18,9 @@ average launch duration.  One rank: HIP events recorded on the world's
 stream (torch's current stream) around the timed region, which is exactly K
 graph-replayed step-kernel launches, / K.  Several ranks: an event pair
 around each step-kernel launch over a second run of K steps.
-cpu_baseline: the oracle (C restatement of the reference arithmetic, one
-core) on rank 0 at N=1 over the full C2 scene for 2,000 steps.
+cpu_baseline: the oracle (C restatement of the reference arithmetic) on rank 0
+at N=1 over the full C2 scene for 2,000 steps, on the GPU's host-core share
+(OMP_NUM_THREADS, 16 on the GPU box) and on one core.
 """
 from __future__ import annotations
 
@@ -59,18 +60,26 @@ def make_scene(cfg: str, P: int):
 
 
 def cpu_baseline(cfg: str, steps: int):
-    """Oracle (C restatement, 1 thread) on the single-GPU scene; returns dict."""
+    """Oracle (C restatement of the reference arithmetic) on the single-GPU
+    scene, on all of this GPU's host-core share (OpenMP over bodies) and on
+    one core; returns the cpu_baseline dict."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     sc, _ = make_scene(cfg, 1)
     osc = O.OracleScene(sc)
-    t0 = time.perf_counter()
-    O.step(osc, sc.qpos0, sc.qvel0, steps)
-    dt = time.perf_counter() - t0
-    return {"value": sc.n * steps / dt, "unit": "body-steps/s", "cores": 1, "kind": "port",
+    cores = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    rates = {}
+    for th in (cores, 1):
+        O.set_threads(th)
+        t0 = time.perf_counter()
+        O.step(osc, sc.qpos0, sc.qvel0, steps)
+        rates[th] = (sc.n * steps / (time.perf_counter() - t0), time.perf_counter() - t0)
+    return {"value": rates[cores][0], "unit": "body-steps/s", "cores": cores, "kind": "port",
+            "value_1core": rates[1][0],
             "sample": f"oracle/rb_oracle.c (C restatement of collision.py/physics_utils.py/"
-                      f"multi_sphere_bounce.py arithmetic) on the full {cfg} scene, {sc.n} bodies x "
-                      f"{steps} steps from t=0, 1 thread, {dt:.1f} s"}
+                      f"multi_sphere_bounce.py arithmetic, bit-identical to the GPU path) on the full {cfg} "
+                      f"scene, {sc.n} bodies x {steps} steps from t=0: {cores} OpenMP threads "
+                      f"{rates[cores][1]:.1f} s, 1 thread {rates[1][1]:.1f} s"}
 
 
 def traffic_from_profiles(cfg: str, dtype: str):

@@ -33,7 +33,7 @@ class SceneDesc(C.Structure):
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB_PATH) or \
             os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f))
-                                             for f in ("rb_oracle.c", "rb_oracle_impl.h")):
+                                             for f in ("rb_oracle.c", "rb_oracle_impl.h", "Makefile")):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -53,8 +53,20 @@ def lib():
             getattr(L, f"rbo_step_{sfx}").argtypes = [P, P, P, P, C.c_int64, C.c_double, C.c_double,
                                                       C.c_double, C.c_double, P, P, P, P, C.c_int64, P]
             getattr(L, f"rbo_contacts_{sfx}").argtypes = [P, P, P, P, P, P, P, P, C.c_int64, P]
+        L.rbo_set_threads.argtypes = [C.c_int]
+        L.rbo_get_threads.restype = C.c_int
         _lib = L
+        set_threads(int(os.environ.get("RBO_THREADS", "1")))
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads of the oracle's per-body loops (default 1, or RBO_THREADS)."""
+    lib().rbo_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return lib().rbo_get_threads()
 
 
 def _ptr(a):

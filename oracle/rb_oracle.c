@@ -24,6 +24,7 @@
  * (SURVEY §4), which the golden trajectory reproduces.
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -54,4 +55,8 @@
 #undef SQRT
 #undef FABS
 
-const char *rbo_version(void) { return "rb_oracle 1 (test infrastructure)"; }
+const char *rbo_version(void) { return "rb_oracle 2 (test infrastructure)"; }
+
+/* OpenMP threads for the per-body loops (the CPU baseline's core count). */
+void rbo_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+int rbo_get_threads(void) { return omp_get_max_threads(); }

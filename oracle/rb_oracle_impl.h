@@ -316,10 +316,13 @@ static REAL FN(bound_radius)(const rb_scene_desc *d, int64_t i) {
     return SQRT((REAL)(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]));
 }
 
-/* Build per-body canonical contact lists for positions pos[N][3] / quats.
- * lists: counts[N], offsets[N+1] into cons (capacity cap). */
+/* Per-body canonical contact lists for positions pos[N][3] / quats: body i's
+ * contacts are cons[i * stride + t], t < counts[i] (stride = 4 * n_planes +
+ * max_partners bounds them).  Bodies are independent after the cell sort
+ * (OpenMP over bodies when built with -fopenmp; results do not depend on the
+ * thread count). */
 static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL *quat,
-                            int32_t *counts, int64_t *offs, FN(rbo_contact) *cons, int64_t cap) {
+                            int32_t *counts, FN(rbo_contact) *cons, int64_t stride) {
     const int64_t N = d->n_bodies;
     const int maxp = d->max_partners > 0 ? d->max_partners : 16;
     REAL rmax = 0;
@@ -327,8 +330,7 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
     const REAL cs = rmax > 0 ? (REAL)2 * rmax * (REAL)1.001 : (REAL)1;
     FN(cellrec) *cells = (FN(cellrec) *)malloc(sizeof(FN(cellrec)) * (size_t)(N > 0 ? N : 1));
     int64_t *ix = (int64_t *)malloc(sizeof(int64_t) * 3 * (size_t)(N > 0 ? N : 1));
-    int64_t *plist = (int64_t *)malloc(sizeof(int64_t) * (size_t)(maxp + 1));
-    if (!cells || !ix || !plist) { free(cells); free(ix); free(plist); return RB_ENOMEM; }
+    if (!cells || !ix) { free(cells); free(ix); return RB_ENOMEM; }
     int rc = RB_OK;
     for (int64_t i = 0; i < N; ++i) {
         for (int k = 0; k < 3; ++k) {
@@ -340,10 +342,12 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
         cells[i].id = i;
     }
     qsort(cells, (size_t)N, sizeof(FN(cellrec)), FN(cell_cmp));
-    int64_t off = 0;
+#pragma omp parallel for schedule(dynamic, 256)
     for (int64_t i = 0; i < N; ++i) {
-        offs[i] = off;
+        int64_t plist[33];
+        int64_t off = i * stride;
         int32_t cnt = 0;
+        int brc = RB_OK;
         const REAL *ci = pos + 3 * i;
         /* planes first, plane order */
         for (int p = 0; p < d->n_planes; ++p) {
@@ -358,7 +362,6 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
                 nc = FN(plane_box)(pn, pp, ci, M, h, tmp);
             }
             for (int t = 0; t < nc; ++t) {
-                if (off >= cap) { rc = RB_EOVERFLOW; goto done; }
                 tmp[t].partner = -1 - p;
                 cons[off++] = tmp[t];
                 ++cnt;
@@ -376,21 +379,21 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
                         int64_t mid = (lo + hi) / 2;
                         if (FN(cell_cmp)(&cells[mid], &probe) < 0) lo = mid + 1; else hi = mid;
                     }
-                    for (int64_t t = lo; t < N && cells[t].key == probe.key; ++t) {
+                    for (int64_t t = lo; t < N && cells[t].key == probe.key && !brc; ++t) {
                         const int64_t j = cells[t].id;
                         if (j == i) continue;
                         const REAL *cj = pos + 3 * j;
                         if (d->kind[i] != RB_BODY_SPHERE || d->kind[j] != RB_BODY_SPHERE) {
                             REAL dd[3] = {ci[0] - cj[0], ci[1] - cj[1], ci[2] - cj[2]};
                             const REAL bi = FN(bound_radius)(d, i), bj = FN(bound_radius)(d, j);
-                            if (SQRT(FN(mj_dot3)(dd, dd)) <= bi + bj) { rc = RB_EUNSUPPORTED; goto done; }
+                            if (SQRT(FN(mj_dot3)(dd, dd)) <= bi + bj) brc = RB_EUNSUPPORTED;
                             continue;
                         }
                         const int64_t g1 = i < j ? i : j, g2 = i < j ? j : i;
                         FN(rbo_contact) con;
                         if (!FN(sphere_sphere)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2,
                                                (REAL)d->size[3 * g2], &con)) continue;
-                        if (np_ >= maxp) { rc = RB_EOVERFLOW; goto done; }
+                        if (np_ >= maxp) { brc = RB_EOVERFLOW; break; }
                         /* insertion into ascending id order */
                         int s = np_++;
                         while (s > 0 && plist[s - 1] > j) { plist[s] = plist[s - 1]; --s; }
@@ -403,15 +406,17 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
             FN(rbo_contact) con;
             FN(sphere_sphere)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2, (REAL)d->size[3 * g2], &con);
             con.partner = (int32_t)j;
-            if (off >= cap) { rc = RB_EOVERFLOW; goto done; }
             cons[off++] = con;
             ++cnt;
         }
         counts[i] = cnt;
+        if (brc) {
+#pragma omp critical
+            if (rc == RB_OK) rc = brc;
+        }
     }
-    offs[N] = off;
 done:
-    free(cells); free(ix); free(plist);
+    free(cells); free(ix);
     return rc;
 }
 
@@ -427,15 +432,14 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
     const int64_t N = d->n_bodies;
     const int maxp = d->max_partners > 0 ? d->max_partners : 16;
     const REAL dt = (REAL)dt_, e = (REAL)e_, mu = (REAL)mu_, thr = (REAL)thr_;
-    const int64_t cap = N * (int64_t)(4 * d->n_planes + maxp) + 1;
+    const int64_t stride = 4 * (int64_t)d->n_planes + maxp;
     REAL *pos = (REAL *)calloc(3 * (size_t)(N + 1), sizeof(REAL));
     REAL *quat = (REAL *)calloc(4 * (size_t)(N + 1), sizeof(REAL));
     REAL *vel = (REAL *)malloc(sizeof(REAL) * 6 * (size_t)(N + 1));
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N + 1));
-    int64_t *offs = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
-    FN(rbo_contact) *cons = (FN(rbo_contact) *)malloc(sizeof(FN(rbo_contact)) * (size_t)cap);
+    FN(rbo_contact) *cons = (FN(rbo_contact) *)malloc(sizeof(FN(rbo_contact)) * (size_t)(N * stride + 1));
     int rc = RB_OK;
-    if (!pos || !quat || !vel || !counts || !offs || !cons) { rc = RB_ENOMEM; goto out; }
+    if (!pos || !quat || !vel || !counts || !cons) { rc = RB_ENOMEM; goto out; }
     for (int64_t i = 0; i < N; ++i) {
         for (int k = 0; k < 3; ++k) pos[3 * i + k] = (REAL)qpos[7 * i + k];
         for (int k = 0; k < 4; ++k) quat[4 * i + k] = (REAL)qpos[7 * i + 3 + k];
@@ -443,8 +447,9 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
     }
     REAL g[3] = {(REAL)d->gravity[0], (REAL)d->gravity[1], (REAL)d->gravity[2]};
     for (int64_t step = 0; step < nsteps; ++step) {
-        rc = FN(gen_contacts)(d, pos, quat, counts, offs, cons, cap);   /* mj_forward */
+        rc = FN(gen_contacts)(d, pos, quat, counts, cons, stride);   /* mj_forward */
         if (rc) goto out;
+#pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < N; ++i) {
             const REAL m = (REAL)d->mass[i];
             const REAL I[3] = {(REAL)d->inertia[3 * i], (REAL)d->inertia[3 * i + 1], (REAL)d->inertia[3 * i + 2]};
@@ -464,7 +469,7 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
                 FN(np_matvec3)(invI, tdt, dw);
                 for (int k = 0; k < 3; ++k) w[k] = w[k] + dw[k];
             }
-            for (int64_t c = offs[i]; c < offs[i] + counts[i]; ++c) {  /* :72-88 */
+            for (int64_t c = i * stride; c < i * stride + counts[i]; ++c) {  /* :72-88 */
                 const FN(rbo_contact) *cc = cons + c;
                 if (!(cc->dist < 0)) continue;                       /* :74 (NaN too) */
                 if (FABS(cc->dist) < thr) continue;                  /* :79-80 */
@@ -499,7 +504,7 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
         int64_t t = 0;
         for (int64_t i = 0; i < N; ++i) {
             out_counts[i] = counts[i];
-            for (int64_t c = offs[i]; c < offs[i] + counts[i]; ++c, ++t) {
+            for (int64_t c = i * stride; c < i * stride + counts[i]; ++c, ++t) {
                 if (t < out_cap) {
                     out_partner[t] = cons[c].partner;
                     out_kind[t] = cons[c].kind;
@@ -511,7 +516,7 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
         if (t > out_cap) rc = RB_EOVERFLOW;
     }
 out:
-    free(pos); free(quat); free(vel); free(counts); free(offs); free(cons);
+    free(pos); free(quat); free(vel); free(counts); free(cons);
     return rc;
 }
 
@@ -522,24 +527,23 @@ int FN(rbo_contacts)(const rb_scene_desc *d, const double *qpos, int32_t *out_co
                      double *out_frame, int64_t out_cap, int64_t *out_total) {
     const int64_t N = d->n_bodies;
     const int maxp = d->max_partners > 0 ? d->max_partners : 16;
-    const int64_t cap = N * (int64_t)(4 * d->n_planes + maxp) + 1;
+    const int64_t stride = 4 * (int64_t)d->n_planes + maxp;
     REAL *pos = (REAL *)calloc(3 * (size_t)(N + 1), sizeof(REAL));
     REAL *quat = (REAL *)calloc(4 * (size_t)(N + 1), sizeof(REAL));
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N + 1));
-    int64_t *offs = (int64_t *)malloc(sizeof(int64_t) * (size_t)(N + 1));
-    FN(rbo_contact) *cons = (FN(rbo_contact) *)malloc(sizeof(FN(rbo_contact)) * (size_t)cap);
+    FN(rbo_contact) *cons = (FN(rbo_contact) *)malloc(sizeof(FN(rbo_contact)) * (size_t)(N * stride + 1));
     int rc = RB_OK;
-    if (!pos || !quat || !counts || !offs || !cons) { rc = RB_ENOMEM; goto out; }
+    if (!pos || !quat || !counts || !cons) { rc = RB_ENOMEM; goto out; }
     for (int64_t i = 0; i < N; ++i) {
         for (int k = 0; k < 3; ++k) pos[3 * i + k] = (REAL)qpos[7 * i + k];
         for (int k = 0; k < 4; ++k) quat[4 * i + k] = (REAL)qpos[7 * i + 3 + k];
     }
-    rc = FN(gen_contacts)(d, pos, quat, counts, offs, cons, cap);
+    rc = FN(gen_contacts)(d, pos, quat, counts, cons, stride);
     if (rc) goto out;
     int64_t t = 0;
     for (int64_t i = 0; i < N; ++i) {
         out_counts[i] = counts[i];
-        for (int64_t c = offs[i]; c < offs[i] + counts[i]; ++c, ++t) {
+        for (int64_t c = i * stride; c < i * stride + counts[i]; ++c, ++t) {
             if (t >= out_cap) continue;
             out_partner[t] = cons[c].partner;
             out_kind[t] = cons[c].kind;
@@ -553,7 +557,7 @@ int FN(rbo_contacts)(const rb_scene_desc *d, const double *qpos, int32_t *out_co
     *out_total = t;
     if (t > out_cap) rc = RB_EOVERFLOW;
 out:
-    free(pos); free(quat); free(counts); free(offs); free(cons);
+    free(pos); free(quat); free(counts); free(cons);
     return rc;
 }
 

@@ -106,3 +106,25 @@ def test_oracle_rejects_box_pairs(oracle):
     sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)    # cubes overlapping
     with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
         oracle.step(oracle.OracleScene(sc), sc.qpos0, sc.qvel0, 1)
+
+
+def test_oracle_thread_count_invariant(oracle):
+    """The CPU baseline runs the oracle with OpenMP over bodies: its results
+    must not depend on the thread count (bodies are independent within a
+    step: Jacobi across bodies, multi_sphere_bounce.py:43-46)."""
+    from rbhip import scenes
+    sc = scenes.flat_spheres(24, 24, seed=3)
+    osc = oracle.OracleScene(sc)
+    out = {}
+    try:
+        for th in (1, 3, 8):
+            oracle.set_threads(th)
+            out[th] = oracle.step(osc, sc.qpos0, sc.qvel0, 80, record=True)
+    finally:
+        oracle.set_threads(1)
+    q1, v1, c1 = out[1]
+    for th in (3, 8):
+        q, v, c = out[th]
+        assert np.array_equal(q, q1) and np.array_equal(v, v1)
+        for a, b in zip(c, c1):
+            assert np.array_equal(a, b)
