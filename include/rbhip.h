@@ -56,6 +56,10 @@ extern "C" {
 #define RB_NORMAL_ORIENTED 0
 #define RB_NORMAL_RAW      1
 
+/* contact laws (rb_set_contact_law) */
+#define RB_LAW_MUJOCO    0    /* the per-body Gauss-Seidel law of collision.py / multi_sphere_bounce.py (default) */
+#define RB_LAW_BALLS     1    /* the symmetric two-ball law of ball_collision.py */
+
 /* contact kinds reported by rb_get_contacts */
 #define RB_CK_PLANE_SPHERE   0
 #define RB_CK_PLANE_BOX0     1   /* 1 + corner index (0..7, corner bits i&1,i&2,i&4) */
@@ -149,6 +153,20 @@ int rb_shard_exchange_done(rb_world *w);
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems,
                    int32_t *elem_bytes);
 
+/* ---- the two-ball law -------------------------------------------------- */
+/* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
+ * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;
+ * ground contact against z = 0 when z < r (impulse, then z = r); ball-ball
+ * contact when |p_b - p_a| < r_a + r_b + tol with the full-effective-mass
+ * impulse compute_collision_impulse (ball_collision.py:53-68) and half-overlap
+ * position correction; x += v dt; quaternions untouched.  Two balls step
+ * exactly as the reference; N balls evaluate every pair from the post-ground
+ * state of both and accumulate per ball in ascending partner id.  Requires
+ * spheres only, world_size 1, and either no plane or exactly the ground
+ * plane (normal (0,0,1) through the origin); tol >= 0 (the reference: 0.01).
+ * rb_step's contact_threshold is ignored under this law. */
+int rb_set_contact_law(rb_world *w, int32_t law, double tol);
+
 /* ---- parity support ---------------------------------------------------- */
 /* Record the contact list generated during the most recent step (off by
  * default: recording costs HBM traffic).  Canonical per-body order: plane
@@ -172,6 +190,11 @@ int rb_kat_impulse(int32_t device, int32_t dtype, int64_t n, const double *in,
                    double *out);
 int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in,
                    double *out);
+/* rb_kat_pair_impulse: per case in[27] = m, e, mu, v[3], w[3], r[3], n[3],
+ * I_inv[9] (row-major) -> out[3] = impulse: compute_collision_impulse
+ * (ball_collision.py:53-68). */
+int rb_kat_pair_impulse(int32_t device, int32_t dtype, int64_t n, const double *in,
+                        double *out);
 /* rb_kat_apply: apply_impulse_friction alone (physics_utils.py:25-49) with
  * caller-given impulses: in[26] = m, v[3], w[3], r[3], n[3], jn, jt[3],
  * inertia_world[9] -> out[6] = v'[3], w'[3]. */

@@ -33,7 +33,8 @@ class SceneDesc(C.Structure):
 def build(force: bool = False) -> str:
     if force or not os.path.exists(LIB_PATH) or \
             os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f))
-                                             for f in ("rb_oracle.c", "rb_oracle_impl.h", "Makefile")):
+                                             for f in ("rb_oracle.c", "rb_oracle_impl.h", "rb_oracle_pairs.h",
+                                                       "Makefile")):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -53,6 +54,9 @@ def lib():
             getattr(L, f"rbo_step_{sfx}").argtypes = [P, P, P, P, C.c_int64, C.c_double, C.c_double,
                                                       C.c_double, C.c_double, P, P, P, P, C.c_int64, P]
             getattr(L, f"rbo_contacts_{sfx}").argtypes = [P, P, P, P, P, P, P, P, C.c_int64, P]
+            getattr(L, f"rbo_kat_pair_impulse_{sfx}").argtypes = [C.c_int64, P, P]
+            getattr(L, f"rbo_pair_step_{sfx}").argtypes = [P, P, P, C.c_int64, C.c_double, C.c_double,
+                                                           C.c_double, C.c_double, P, P, C.c_int64, P]
         L.rbo_set_threads.argtypes = [C.c_int]
         L.rbo_get_threads.restype = C.c_int
         _lib = L
@@ -159,3 +163,35 @@ def contacts(osc: OracleScene, qpos, dtype: str = "f64"):
         raise RuntimeError(f"oracle rbo_contacts failed: {RB_ENAMES.get(rc, rc)}")
     t = tot.value
     return cnt, par[:t], kin[:t], dis[:t], pos[:t], frm[:t]
+
+
+def kat_pair_impulse(inp: np.ndarray, dtype: str = "f64") -> np.ndarray:
+    """ball_collision.py:53-68 per row: in[27] = m, e, mu, v, w, r, n, I_inv(9) -> impulse(3)."""
+    inp = np.ascontiguousarray(inp, np.float64)
+    out = np.zeros((inp.shape[0], 3))
+    getattr(lib(), f"rbo_kat_pair_impulse_{dtype}")(inp.shape[0], _ptr(inp), _ptr(out))
+    return out
+
+
+def pair_step(osc: OracleScene, qpos, qvel, nsteps: int, dt=None, restitution=None, friction=None,
+              tol: float = 0.01, dtype: str = "f64", record: bool = False):
+    """The ball law (ball_collision.py:73-125, Jacobi over pairs for N > 2):
+    returns (qpos, qvel[, (counts, partners)])."""
+    sc = osc.sc
+    dt = sc.dt if dt is None else dt
+    restitution = sc.restitution if restitution is None else restitution
+    friction = sc.friction if friction is None else friction
+    q = np.ascontiguousarray(qpos, np.float64).copy()
+    v = np.ascontiguousarray(qvel, np.float64).copy()
+    n = sc.n
+    cap = n * 32 + 1
+    cnt = np.zeros(n, np.int32) if record else None
+    par = np.zeros(cap, np.int32) if record else None
+    tot = C.c_int64(0)
+    rc = getattr(lib(), f"rbo_pair_step_{dtype}")(C.byref(osc.desc), _ptr(q), _ptr(v), nsteps, dt, restitution,
+                                                 friction, tol, _ptr(cnt), _ptr(par), cap, C.byref(tot))
+    if rc != 0:
+        raise RuntimeError(f"oracle rbo_pair_step failed: {RB_ENAMES.get(rc, rc)}")
+    if record:
+        return q, v, (cnt, par[:tot.value])
+    return q, v

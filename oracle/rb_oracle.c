@@ -14,6 +14,9 @@
  *                      timestep_integration time_integeration.py:13-72, and the N-body
  *                      driver custom_step_multi_sphere multi_sphere_bounce.py:42-92
  *                      (SURVEY D1/D2 fixed: body k -> qpos[7k], contacts by body index)
+ *   rbo_pair_step      the two-ball law of src/simulation/ball_collision.py:39-125
+ *                      (compute_collision_impulse, step_with_custom_collisions),
+ *                      generalised to N balls (rb_oracle_pairs.h)
  *   gen_contacts       MuJoCo mj_forward's collision pipeline for plane-sphere,
  *                      plane-box and sphere-sphere (third-party C, not vendored,
  *                      unpinned; restated from MuJoCo's published primitives).
@@ -37,6 +40,7 @@
 #define SQRT sqrt
 #define FABS fabs
 #include "rb_oracle_impl.h"
+#include "rb_oracle_pairs.h"
 #undef REAL
 #undef SFX
 #undef FMA
@@ -49,6 +53,7 @@
 #define SQRT sqrtf
 #define FABS fabsf
 #include "rb_oracle_impl.h"
+#include "rb_oracle_pairs.h"
 #undef REAL
 #undef SFX
 #undef FMA

@@ -561,6 +561,4 @@ out:
     return rc;
 }
 
-#undef FN
-#undef CAT
-#undef CAT_
+/* FN / CAT stay defined: rb_oracle_pairs.h follows and undefines them */

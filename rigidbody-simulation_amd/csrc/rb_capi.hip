@@ -75,11 +75,18 @@ struct rb_world {
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};
     double inv_cs = 1.0;
+    double rmax = 0.0;             // largest bounding radius
+    bool all_spheres = true;
+    // contact law (rb_set_contact_law)
+    int32_t law = RB_LAW_MUJOCO;
+    double tol = 0.01;
+    double prm_dt = 0, prm_e = 0, prm_mu = 0;   // the ground phase held in the snapshots (two-ball law)
     int64_t H = 4096;
     int64_t bytes_per_body_step = 0;
     // device memory
     void *snap[2] = {};        // [Npad] Snap<T>: (x, y, z, bound radius), ping-pong
-    void *state = nullptr;     // 10 x S  (qw qx qy qz vx vy vz wx wy wz)
+    void *state = nullptr;     // 13 x S  (qw qx qy qz vx vy vz wx wy wz px py pz)
+    void *vel[2] = {};         // two-ball law: [Npad] Vel<T>, ping-pong with the snapshots
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
@@ -135,8 +142,9 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.lo = (int32_t)w->lo;
     p.S = (int32_t)w->S;
     T *st = dp<T>(w->state, 0);
-    T **f[10] = {&p.st.qw, &p.st.qx, &p.st.qy, &p.st.qz, &p.st.vx, &p.st.vy, &p.st.vz, &p.st.wx, &p.st.wy, &p.st.wz};
-    for (int k = 0; k < 10; ++k) *f[k] = st + k * w->S;
+    T **f[13] = {&p.st.qw, &p.st.qx, &p.st.qy, &p.st.qz, &p.st.vx, &p.st.vy, &p.st.vz, &p.st.wx, &p.st.wy, &p.st.wz,
+                 &p.st.px, &p.st.py, &p.st.pz};
+    for (int k = 0; k < 13; ++k) *f[k] = st + k * w->S;
     const T *cst = dp<T>(w->consts, 0);
     p.cs.mass = cst; p.cs.ix = cst + w->Npad; p.cs.iy = cst + 2 * w->Npad; p.cs.iz = cst + 3 * w->Npad;
     p.cs.sx = cst + 4 * w->Npad; p.cs.sy = cst + 5 * w->Npad; p.cs.sz = cst + 6 * w->Npad;
@@ -159,6 +167,12 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.err = w->err;
     p.plist = w->plist;
     p.plist_cnt = w->plist_cnt;
+    if (w->vel[0]) {
+        p.vel_cur = dp<Vel<T>>(w->vel[sp], 0);
+        p.vel_next = dp<Vel<T>>(w->vel[1 - sp], 0);
+    }
+    p.tol = (T)w->tol;
+    p.ground = w->n_planes > 0;
     if (w->record) {
         p.rec_count = w->rec_count; p.rec_partner = w->rec_partner; p.rec_kind = w->rec_kind;
         p.rec_dist = dp<T>(w->rec_dist, 0);
@@ -179,19 +193,43 @@ template <typename T> InsertParams<T> make_insert(rb_world *w, int sp, int ph, i
     return ip;
 }
 
-// (re)build the current table from every body's snapshot
-int prime(rb_world *w) {
+// (re)build the current table from every body's snapshot; under the
+// two-ball law first run the coming step's ground phase from the true state
+// (it depends on dt, e, mu: remembered, and re-primed when they change)
+int prime(rb_world *w, double dt = 0, double e = 0, double mu = 0) {
+    if (w->law == RB_LAW_BALLS) {
+        hipError_t r;
+        if (w->dtype == RB_F64) {
+            StepParams<double> p = make_step<double>(w, w->c, dt, e, mu, 0.0, false);
+            p.snap_next = dp<Snap<double>>(w->snap[w->sp()], 0);
+            p.vel_next = dp<Vel<double>>(w->vel[w->sp()], 0);
+            r = launch_ball_prime<double>(p, w->stream);
+        } else {
+            StepParams<float> p = make_step<float>(w, w->c, dt, e, mu, 0.0, false);
+            p.snap_next = dp<Snap<float>>(w->snap[w->sp()], 0);
+            p.vel_next = dp<Vel<float>>(w->vel[w->sp()], 0);
+            r = launch_ball_prime<float>(p, w->stream);
+        }
+        HIPCHK(r);
+        w->prm_dt = dt; w->prm_e = e; w->prm_mu = mu;
+    }
     for (int k = 0; k < 3; ++k) HIPCHK(hipMemsetAsync(w->cnt[k], 0, sizeof(int32_t) * w->H, w->stream));
-    hipError_t e = w->dtype == RB_F64
-                       ? launch_insert<double>(make_insert<double>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream)
-                       : launch_insert<float>(make_insert<float>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream);
-    HIPCHK(e);
+    hipError_t ie = w->dtype == RB_F64
+                        ? launch_insert<double>(make_insert<double>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream)
+                        : launch_insert<float>(make_insert<float>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream);
+    HIPCHK(ie);
     w->primed = true;
     return RB_OK;
 }
 
 int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, double mu, double thr) {
     hipError_t r;
+    if (w->law == RB_LAW_BALLS) {
+        if (w->dtype == RB_F64) r = launch_ball_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, s);
+        else r = launch_ball_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, s);
+        HIPCHK(r);
+        return RB_OK;
+    }
     const bool coop = w->n_local <= w->coop_max;
     if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, coop, s);
     else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, coop, s);
@@ -251,7 +289,10 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
     HIPCHK(hipSetDevice(w->device));
-    if (!w->primed) { int rc = prime(w); if (rc) return rc; }
+    if (!w->primed || (w->law == RB_LAW_BALLS && (dt != w->prm_dt || e != w->prm_e || mu != w->prm_mu))) {
+        int rc = prime(w, dt, e, mu);
+        if (rc) return rc;
+    }
     if (w->timing) {
         // eager launches, each bracketed by events on the launch stream
         for (int64_t k = 0; k < nsteps; ++k) {
@@ -307,11 +348,12 @@ int upload_state(rb_world *w, const double *qpos, const double *qvel, const doub
         for (int d = 0; d < 3; ++d) sn[(size_t)(4 * b + d)] = (T)qpos[7 * b + d];
         sn[(size_t)(4 * b + 3)] = (T)bound[b];
     }
-    std::vector<T> st((size_t)10 * w->S, T(0));
+    std::vector<T> st((size_t)13 * w->S, T(0));
     for (int64_t l = 0; l < w->n_local; ++l) {
         const int64_t b = w->lo + l;
         for (int d = 0; d < 4; ++d) st[(size_t)(d * w->S + l)] = (T)qpos[7 * b + 3 + d];
         for (int d = 0; d < 6; ++d) st[(size_t)((4 + d) * w->S + l)] = (T)qvel[6 * b + d];
+        for (int d = 0; d < 3; ++d) st[(size_t)((10 + d) * w->S + l)] = (T)qpos[7 * b + d];
     }
     HIPCHK(hipMemcpyAsync(w->snap[w->sp()], sn.data(), sizeof(T) * sn.size(), hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(w->state, st.data(), sizeof(T) * st.size(), hipMemcpyHostToDevice, w->stream));
@@ -321,7 +363,7 @@ int upload_state(rb_world *w, const double *qpos, const double *qvel, const doub
 
 template <typename T>
 int download_state(rb_world *w, double *qpos, double *qvel) {
-    std::vector<T> sn((size_t)4 * w->S), st((size_t)10 * w->S);
+    std::vector<T> sn((size_t)4 * w->S), st((size_t)13 * w->S);
     HIPCHK(hipMemcpyAsync(sn.data(), dp<T>(w->snap[w->sp()], 4 * w->lo), sizeof(T) * sn.size(),
                           hipMemcpyDeviceToHost, w->stream));
     HIPCHK(hipMemcpyAsync(st.data(), w->state, sizeof(T) * st.size(), hipMemcpyDeviceToHost, w->stream));
@@ -329,7 +371,11 @@ int download_state(rb_world *w, double *qpos, double *qvel) {
     for (int64_t l = 0; l < w->n_local; ++l) {
         const int64_t b = w->lo + l;
         if (qpos) {
-            for (int d = 0; d < 3; ++d) qpos[7 * b + d] = (double)sn[(size_t)(4 * l + d)];
+            // positions: the snapshot, or under the two-ball law (whose
+            // snapshot is post-ground) the true positions px, py, pz
+            for (int d = 0; d < 3; ++d)
+                qpos[7 * b + d] = w->law == RB_LAW_BALLS ? (double)st[(size_t)((10 + d) * w->S + l)]
+                                                          : (double)sn[(size_t)(4 * l + d)];
             for (int d = 0; d < 4; ++d) qpos[7 * b + 3 + d] = (double)st[(size_t)(d * w->S + l)];
         }
         if (qvel)
@@ -360,8 +406,10 @@ int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &boun
         c[(size_t)(7 * w->Npad + b)] = (T)bound[(size_t)b];
     }
     // cell = 2 x the largest contact reach (2 x 2 rmax): the 2x2x2 query
+    w->rmax = rmax;
     const double cs = rmax > 0 ? 4.0 * rmax * 1.001 : 1.0;
     w->inv_cs = 1.0 / cs;
+    for (int64_t b = 0; b < w->N; ++b) w->all_spheres = w->all_spheres && d->kind[b] == RB_BODY_SPHERE;
     HIPCHK(hipMemcpy(w->consts, c.data(), sizeof(T) * c.size(), hipMemcpyHostToDevice));
     std::vector<int32_t> k((size_t)w->Npad, 0);
     for (int64_t b = 0; b < w->N; ++b) k[(size_t)b] = d->kind[b];
@@ -375,7 +423,7 @@ void free_world(rb_world *w) {
     drop_graphs(w);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
-                    w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->err, w->rec_count, w->rec_partner, w->rec_kind,
+                    w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -454,7 +502,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
             return bail(fail(RB_ENOMEM, "hipMalloc(%lld) failed", (long long)(bytes)));          \
     } while (0)
     for (int k = 0; k < 2; ++k) ALLOC(w->snap[k], (size_t)w->esz * 4 * w->Npad);
-    ALLOC(w->state, (size_t)w->esz * 10 * w->S);
+    ALLOC(w->state, (size_t)w->esz * 13 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
     for (int k = 0; k < 3; ++k) ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
@@ -482,7 +530,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->stream = w->own_stream;
     if (hipMemset(w->snap[0], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
         hipMemset(w->snap[1], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
-        hipMemset(w->state, 0, (size_t)w->esz * 10 * w->S) != hipSuccess ||
+        hipMemset(w->state, 0, (size_t)w->esz * 13 * w->S) != hipSuccess ||
         hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipMemset failed"));
     std::vector<double> bound;
@@ -560,6 +608,7 @@ int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double 
 
 int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
     if (!w) return fail(RB_EINVAL, "null world");
+    if (w->law != RB_LAW_MUJOCO) return fail(RB_EUNSUPPORTED, "sharded stepping supports the default contact law only");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0)) return fail(RB_EINVAL, "invalid step parameters");
     HIPCHK(hipSetDevice(w->device));
     if (!w->primed) { int rc = prime(w); if (rc) return rc; }
@@ -660,6 +709,7 @@ static int kat_common(int32_t device, int32_t dtype, int64_t n, const double *in
     if (e == hipSuccess) {
         if (which == 1) e = dtype == RB_F64 ? launch_kat_inertia<double>(n, din, dout, nullptr) : launch_kat_inertia<float>(n, din, dout, nullptr);
         else if (which == 2) e = dtype == RB_F64 ? launch_kat_apply<double>(n, din, dout, nullptr) : launch_kat_apply<float>(n, din, dout, nullptr);
+        else if (which == 3) e = dtype == RB_F64 ? launch_kat_pair_impulse<double>(n, din, dout, nullptr) : launch_kat_pair_impulse<float>(n, din, dout, nullptr);
         else e = dtype == RB_F64 ? launch_kat_impulse<double>(n, din, dout, nullptr) : launch_kat_impulse<float>(n, din, dout, nullptr);
     }
     if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * nout * n, hipMemcpyDeviceToHost);
@@ -679,6 +729,62 @@ int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in, d
 
 int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
     return kat_common(device, dtype, n, in, out, 26, 6, 2);
+}
+
+int rb_kat_pair_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    return kat_common(device, dtype, n, in, out, 27, 3, 3);
+}
+
+int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (law != RB_LAW_MUJOCO && law != RB_LAW_BALLS) return fail(RB_EINVAL, "unknown contact law %d", law);
+    if (!(tol >= 0) || !(tol < 1e6)) return fail(RB_EINVAL, "tol must be finite and >= 0");
+    if (law == RB_LAW_BALLS) {
+        if (!w->all_spheres) return fail(RB_EUNSUPPORTED, "the two-ball law takes spheres only");
+        if (w->P != 1) return fail(RB_EUNSUPPORTED, "the two-ball law steps unsharded worlds only");
+        const double ground[6] = {0, 0, 1, 0, 0, 0};
+        if (w->n_planes > 1 || (w->n_planes == 1 && memcmp(w->planes[0], ground, sizeof(ground)) != 0))
+            return fail(RB_EUNSUPPORTED, "the two-ball law's only plane is the z = 0 ground (ball_collision.py:88-90)");
+    }
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (law == RB_LAW_BALLS && !w->vel[0]) {
+        const size_t bytes = (size_t)w->esz * 8 * w->Npad;
+        for (int k = 0; k < 2; ++k) {
+            if (hipMalloc(&w->vel[k], bytes) != hipSuccess) return fail(RB_ENOMEM, "hipMalloc(%zu) failed", bytes);
+            HIPCHK(hipMemset(w->vel[k], 0, bytes));
+        }
+    }
+    if (w->law == RB_LAW_BALLS && law == RB_LAW_MUJOCO) {
+        // the default law keeps positions in the snapshot: restore them
+        // from the true positions before the snapshot is read again
+        const size_t esz = (size_t)w->esz;
+        std::vector<char> st(esz * 13 * w->S), sn(esz * 4 * w->Npad);
+        HIPCHK(hipMemcpy(st.data(), w->state, st.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sn.size(), hipMemcpyDeviceToHost));
+        for (int64_t l = 0; l < w->n_local; ++l)
+            for (int d = 0; d < 3; ++d)
+                memcpy(&sn[esz * (4 * (w->lo + l) + d)], &st[esz * ((10 + d) * w->S + l)], esz);
+        HIPCHK(hipMemcpy(w->snap[w->sp()], sn.data(), sn.size(), hipMemcpyHostToDevice));
+    } else if (w->law == RB_LAW_MUJOCO && law == RB_LAW_BALLS) {
+        // the other way: the true positions from the snapshot
+        const size_t esz = (size_t)w->esz;
+        std::vector<char> st(esz * 13 * w->S), sn(esz * 4 * w->Npad);
+        HIPCHK(hipMemcpy(st.data(), w->state, st.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sn.size(), hipMemcpyDeviceToHost));
+        for (int64_t l = 0; l < w->n_local; ++l)
+            for (int d = 0; d < 3; ++d)
+                memcpy(&st[esz * ((10 + d) * w->S + l)], &sn[esz * (4 * (w->lo + l) + d)], esz);
+        HIPCHK(hipMemcpy(w->state, st.data(), st.size(), hipMemcpyHostToDevice));
+    }
+    w->law = law;
+    w->tol = tol;
+    // cell = 2 x the largest reach: 2 x 2 rmax, or 2 x (2 rmax + tol)
+    const double reach = law == RB_LAW_BALLS ? 2.0 * w->rmax + tol : 2.0 * w->rmax;
+    w->inv_cs = 1.0 / (reach > 0 ? 2.0 * reach * 1.001 : 1.0);
+    drop_graphs(w);
+    w->primed = false;
+    return RB_OK;
 }
 
 int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {

@@ -1,0 +1,228 @@
+// rb_grid.hpp — the spatial-hash broadphase shared by the step kernels
+// (rb_kernels.hip) and the two-ball law (rb_balls.hip): cell and bucket
+// maps, slot claims and publication, bucket reads, the 2x2x2 neighbourhood
+// and the ascending per-body partner list.  Not part of the public interface.
+#pragma once
+
+#include "rb_device.hpp"
+#include "rb_internal.hpp"
+
+// write-through (sc1) stores for everything the next step reads: the lines
+// leave L2 as they are written, so the end-of-kernel L2 writeback has
+// nothing left to flush
+#ifndef RB_WT
+#define RB_WT 0
+#endif
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
+// so block b runs body-block xcd_block(b) and each XCD (own L2) steps one
+// contiguous id range = one spatial region of the scene
+#ifndef RB_XCD_REMAP
+#define RB_XCD_REMAP 0
+#endif
+
+// candidates whose snapshot loads are issued together
+#ifndef RB_QBATCH
+#define RB_QBATCH 4
+#endif
+
+namespace rb {
+
+// diagnostic build only (RB_BOUNDS=1): index checks that report and clamp
+// instead of faulting
+#ifndef RB_BOUNDS
+#define RB_BOUNDS 0
+#endif
+__device__ __forceinline__ int64_t chk(int64_t idx, int64_t n, int line) {
+#if RB_BOUNDS
+    if (idx < 0 || idx >= n) {
+        printf("RB_BOUNDS line %d: index %lld outside [0, %lld) block %d thread %d\n", line, (long long)idx,
+               (long long)n, (int)blockIdx.x, (int)threadIdx.x);
+        return 0;
+    }
+#else
+    (void)n; (void)line;
+#endif
+    return idx;
+}
+#define CHK(idx, n) chk((idx), (n), __LINE__)
+
+constexpr uint32_t N_XCD = 8;
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+#if RB_XCD_REMAP
+    const uint32_t q = nb / N_XCD, r = nb % N_XCD, x = b % N_XCD;
+    return x * q + (x < r ? x : r) + b / N_XCD;
+#else
+    (void)nb;
+    return b;
+#endif
+}
+
+template <typename V> __device__ __forceinline__ void wt_store(V *ptr, V v) {
+#if RB_WT
+    __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *ptr = v;
+#endif
+}
+template <typename T> __device__ __forceinline__ void wt_store(Snap<T> *ptr, const Snap<T> &v) {
+    wt_store(&ptr->x, v.x); wt_store(&ptr->y, v.y); wt_store(&ptr->z, v.z); wt_store(&ptr->r, v.r);
+}
+
+// cell -> bucket: murmur3-finalised hash of the cell coordinates
+__device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, uint32_t hmask) {
+    uint32_t h = (uint32_t)ix * 0x8da6b343u + (uint32_t)iy * 0xd8163841u + (uint32_t)iz * 0xcb1ab31fu;
+    h ^= h >> 16; h *= 0x85ebca6bu;
+    h ^= h >> 13; h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h & hmask;
+}
+
+// cell coordinates; false for non-finite / out-of-range positions
+template <typename T>
+__device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, int32_t &iy, int32_t &iz) {
+    const T fx = x * inv_cs, fy = y * inv_cs, fz = z * inv_cs;
+    const T lim = T(1 << 29);
+    if (!(absval(fx) < lim && absval(fy) < lim && absval(fz) < lim)) return false;
+    ix = (int32_t)__builtin_floor((double)fx);
+    iy = (int32_t)__builtin_floor((double)fy);
+    iz = (int32_t)__builtin_floor((double)fz);
+    return true;
+}
+
+// Append a body (tagged id + snapshot) to the bucket of its cell: one
+// returning atomicAdd claims the slot (claim_slot), the slot is then
+// written (publish_slot).  Split so a caller can put independent work
+// between the two and hide the atomic's round trip.
+struct Claim { uint32_t b; int32_t slot; };      // slot < 0: not inserted
+template <typename T>
+__device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn) {
+    int32_t ix, iy, iz;
+    if (!cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return {0u, -1}; }
+    const uint32_t b = bucket_of(ix, iy, iz, g.hmask);
+    return {b, atomicAdd(tab.cnt + b, 1)};
+}
+template <typename T>
+__device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
+                                             uint32_t tagged_id) {
+    if (c.slot < 0) return;
+    if (c.slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    const int64_t o = CHK((int64_t)c.b * BUCKET_SLOTS + c.slot, RB_BOUNDS ? 1ll << 40 : 0);
+    wt_store(tab.ids + o, tagged_id);
+    if (tab.pos) wt_store(tab.pos + o, sn);
+}
+template <typename T>
+__device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
+                                          uint32_t tagged_id) {
+    publish_slot(tab, err, claim_slot(g, tab, err, sn), sn, tagged_id);
+}
+
+// count (clamped) and the first 4 ids of a bucket, loaded together
+template <typename T>
+__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int32_t &count) {
+    const int32_t c = tab.cnt[CHK(b, RB_BOUNDS ? 1ll << 40 : 0)];
+    const uint4 h = *reinterpret_cast<const uint4 *>(tab.ids + (int64_t)b * BUCKET_SLOTS);
+    count = c < BUCKET_SLOTS ? c : BUCKET_SLOTS;
+    return h;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s) {
+    return s == 0 ? h.x : s == 1 ? h.y : s == 2 ? h.z : s == 3 ? h.w : tab.ids[(int64_t)b * BUCKET_SLOTS + s];
+}
+
+// The 2x2x2 cell neighbourhood: cell size = 2 x the largest contact reach
+// (2 x max bounding diameter), so every partner lies in this body's cell or
+// its neighbour on the nearer side along each axis.
+template <typename T>
+__device__ __forceinline__ bool neighbourhood(const StepParams<T> &p, V3<T> x, int32_t &cx, int32_t &cy, int32_t &cz,
+                                              int32_t &sx, int32_t &sy, int32_t &sz) {
+    if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) return false;
+    sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
+    sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
+    sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
+    return true;
+}
+
+// Insert partner id j into a per-body list kept ascending in LDS.
+template <int MAXP>
+__device__ __forceinline__ void list_insert(int32_t *s_id, int stride, int slot, int32_t &np_, int32_t j,
+                                            bool &overflow) {
+    int pos = np_;
+    while (pos > 0) {
+        const int32_t prev = s_id[(pos - 1) * stride + slot];
+        if (prev == j) return;                       // reached through two hashed cells
+        if (prev < j) break;
+        --pos;
+    }
+    if (np_ >= MAXP) { overflow = true; return; }
+    for (int t = np_; t > pos; --t) s_id[t * stride + slot] = s_id[(t - 1) * stride + slot];
+    s_id[pos * stride + slot] = j;
+    ++np_;
+}
+
+// One lane per body: the 8 bucket counts and the first 4 ids of each bucket
+// are loaded together, then candidates in batches of RB_QBATCH (snapshot
+// loads in flight together); hit(tagged id, snapshot) decides a partner.
+// The partners go to the body's LDS column of s_id in ascending id order.
+// Returns the partner count.
+template <typename T, int MAXP, typename Hit>
+__device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
+                                                  int tid, Hit hit) {
+    constexpr int NB = STEP_BLOCK;
+    int32_t cx, cy, cz, sx, sy, sz;
+    if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) { atomicOr(p.err, ERR_DOMAIN); return 0; }
+    uint32_t b[8];
+    int32_t c[8];
+    uint4 id4[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid.hmask);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) id4[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H), c[k]);
+    int32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int32_t n = c[k];
+#pragma unroll
+        for (int j = 0; j < k; ++j)
+            if (b[j] == b[k]) n = 0;                  // two cells hashed to one bucket: visit once
+        c[k] = n;
+        total += n;
+    }
+    int32_t np_ = 0;
+    bool overflow = false;
+    for (int base = 0; base < total; base += RB_QBATCH) {
+        uint32_t tj[RB_QBATCH];
+        Snap<T> sn[RB_QBATCH];
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u) {
+            int32_t rem = base + u;
+            uint32_t t = (uint32_t)i;
+            int64_t addr = -1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (rem >= 0 && rem < c[k]) {
+                    if (rem == 0) t = id4[k].x;
+                    else if (rem == 1) t = id4[k].y;
+                    else if (rem == 2) t = id4[k].z;
+                    else if (rem == 3) t = id4[k].w;
+                    else addr = (int64_t)b[k] * BUCKET_SLOTS + rem;
+                }
+                rem -= c[k];
+            }
+            if (base + u < total && addr >= 0) t = p.cur.ids[CHK(addr, (int64_t)p.grid.H * BUCKET_SLOTS)];
+            tj[u] = (base + u < total) ? t : (uint32_t)i;
+        }
+        // the id-indexed snapshot: ids are spatially coherent, so a wave's
+        // candidates share lines (cheaper than bucket slots at this scale)
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+#pragma unroll
+        for (int u = 0; u < RB_QBATCH; ++u)
+            if (hit(tj[u], sn[u]))
+                list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
+    }
+    if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
+    return np_;
+}
+
+}  // namespace rb

@@ -40,13 +40,19 @@ template <typename T> struct Table {
 
 constexpr int MAX_PLANES = 8;
 
-// Structure-of-arrays body state of this shard (positions live in the
-// snapshots).
+// Structure-of-arrays body state of this shard.  Positions live in the
+// snapshots, except under the two-ball law, whose snapshots hold the next
+// step's post-ground positions: its true positions are px, py, pz.
 template <typename T> struct BodyState {
     T *qw, *qx, *qy, *qz;
     T *vx, *vy, *vz;
     T *wx, *wy, *wz;
+    T *px, *py, *pz;
 };
+
+// Two-ball law: a ball's post-ground velocity and spin, indexed by global id
+// (ping-pong with the snapshots).
+template <typename T> struct alignas(8 * sizeof(T)) Vel { T vx, vy, vz, wx, wy, wz, pad0, pad1; };
 
 // Per-body constants, global body index (replicated on every rank).
 template <typename T> struct BodyConsts {
@@ -83,6 +89,11 @@ template <typename T> struct StepParams {
     int32_t *err;
     // split form only: sorted partner ids [MAXP][S] and counts [S]
     int32_t *plist, *plist_cnt;
+    // two-ball law only (rb_balls.hip)
+    const Vel<T> *vel_cur;             // post-ground velocity / spin of snap_cur
+    Vel<T> *vel_next;
+    T tol;                             // ball_collision.py:102
+    int32_t ground;                    // the z = 0 ground plane is present
     // optional contact recording ([n_local][maxrec] slots)
     int32_t *rec_count, *rec_partner, *rec_kind;
     T *rec_dist;
@@ -105,6 +116,10 @@ template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStre
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s);
+// two-ball law (rb_balls.hip)
+template <typename T> hipError_t launch_ball_step(const StepParams<T> &p, int maxp, hipStream_t s);
+template <typename T> hipError_t launch_ball_prime(const StepParams<T> &p, hipStream_t s);
+template <typename T> hipError_t launch_kat_pair_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 
 constexpr int STEP_BLOCK = 64;
 

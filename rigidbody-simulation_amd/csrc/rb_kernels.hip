@@ -21,6 +21,7 @@
 //   thread of the same launch writes: Jacobi across bodies, exactly as
 //   multi_sphere_bounce.py:43-46 (one mj_forward per step).
 #include "rb_device.hpp"
+#include "rb_grid.hpp"
 #include "rb_internal.hpp"
 
 // diagnostic builds only (scripts/ablate.py): 1 = skip the sphere-sphere
@@ -46,127 +47,8 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][16];
 #else
 #define STAMP(k) do {} while (0)
 #endif
-// candidates whose snapshot loads are issued together
-#ifndef RB_QBATCH
-#define RB_QBATCH 4
-#endif
-
-// write-through (sc1) stores for everything the next step reads: the lines
-// leave L2 as they are written, so the end-of-kernel L2 writeback has
-// nothing left to flush
-#ifndef RB_WT
-#define RB_WT 0
-#endif
-// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
-// so block b runs body-block xcd_block(b) and each XCD (own L2) steps one
-// contiguous id range = one spatial region of the scene
-#ifndef RB_XCD_REMAP
-#define RB_XCD_REMAP 1
-#endif
 
 namespace rb {
-
-// diagnostic build only (RB_BOUNDS=1): index checks that report and clamp
-// instead of faulting
-#ifndef RB_BOUNDS
-#define RB_BOUNDS 0
-#endif
-__device__ __forceinline__ int64_t chk(int64_t idx, int64_t n, int line) {
-#if RB_BOUNDS
-    if (idx < 0 || idx >= n) {
-        printf("RB_BOUNDS line %d: index %lld outside [0, %lld) block %d thread %d\n", line, (long long)idx,
-               (long long)n, (int)blockIdx.x, (int)threadIdx.x);
-        return 0;
-    }
-#else
-    (void)n; (void)line;
-#endif
-    return idx;
-}
-#define CHK(idx, n) chk((idx), (n), __LINE__)
-
-constexpr uint32_t N_XCD = 8;
-__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
-#if RB_XCD_REMAP
-    const uint32_t q = nb / N_XCD, r = nb % N_XCD, x = b % N_XCD;
-    return x * q + (x < r ? x : r) + b / N_XCD;
-#else
-    (void)nb;
-    return b;
-#endif
-}
-
-template <typename V> __device__ __forceinline__ void wt_store(V *ptr, V v) {
-#if RB_WT
-    __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    *ptr = v;
-#endif
-}
-template <typename T> __device__ __forceinline__ void wt_store(Snap<T> *ptr, const Snap<T> &v) {
-    wt_store(&ptr->x, v.x); wt_store(&ptr->y, v.y); wt_store(&ptr->z, v.z); wt_store(&ptr->r, v.r);
-}
-
-// cell -> bucket: murmur3-finalised hash of the cell coordinates
-__device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, uint32_t hmask) {
-    uint32_t h = (uint32_t)ix * 0x8da6b343u + (uint32_t)iy * 0xd8163841u + (uint32_t)iz * 0xcb1ab31fu;
-    h ^= h >> 16; h *= 0x85ebca6bu;
-    h ^= h >> 13; h *= 0xc2b2ae35u;
-    h ^= h >> 16;
-    return h & hmask;
-}
-
-// cell coordinates; false for non-finite / out-of-range positions
-template <typename T>
-__device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, int32_t &iy, int32_t &iz) {
-    const T fx = x * inv_cs, fy = y * inv_cs, fz = z * inv_cs;
-    const T lim = T(1 << 29);
-    if (!(absval(fx) < lim && absval(fy) < lim && absval(fz) < lim)) return false;
-    ix = (int32_t)__builtin_floor((double)fx);
-    iy = (int32_t)__builtin_floor((double)fy);
-    iz = (int32_t)__builtin_floor((double)fz);
-    return true;
-}
-
-// Append a body (tagged id + snapshot) to the bucket of its cell: one
-// returning atomicAdd claims the slot (claim_slot), the slot is then
-// written (publish_slot).  Split so a caller can put independent work
-// between the two and hide the atomic's round trip.
-struct Claim { uint32_t b; int32_t slot; };      // slot < 0: not inserted
-template <typename T>
-__device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn) {
-    int32_t ix, iy, iz;
-    if (!cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return {0u, -1}; }
-    const uint32_t b = bucket_of(ix, iy, iz, g.hmask);
-    return {b, atomicAdd(tab.cnt + b, 1)};
-}
-template <typename T>
-__device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
-                                             uint32_t tagged_id) {
-    if (c.slot < 0) return;
-    if (c.slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    const int64_t o = CHK((int64_t)c.b * BUCKET_SLOTS + c.slot, RB_BOUNDS ? 1ll << 40 : 0);
-    wt_store(tab.ids + o, tagged_id);
-    if (tab.pos) wt_store(tab.pos + o, sn);
-}
-template <typename T>
-__device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
-                                          uint32_t tagged_id) {
-    publish_slot(tab, err, claim_slot(g, tab, err, sn), sn, tagged_id);
-}
-
-// count (clamped) and the first 4 ids of a bucket, loaded together
-template <typename T>
-__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int32_t &count) {
-    const int32_t c = tab.cnt[CHK(b, RB_BOUNDS ? 1ll << 40 : 0)];
-    const uint4 h = *reinterpret_cast<const uint4 *>(tab.ids + (int64_t)b * BUCKET_SLOTS);
-    count = c < BUCKET_SLOTS ? c : BUCKET_SLOTS;
-    return h;
-}
-template <typename T>
-__device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s) {
-    return s == 0 ? h.x : s == 1 ? h.y : s == 2 ? h.z : s == 3 ? h.w : tab.ids[(int64_t)b * BUCKET_SLOTS + s];
-}
 
 template <typename T>
 __global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
@@ -241,112 +123,28 @@ __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i,
     return sphere_sphere_hit(x, rad, cj, s.r);
 }
 
-// The 2x2x2 cell neighbourhood: cell size = 2 x the largest contact reach
-// (2 x max bounding diameter), so every partner lies in this body's cell or
-// its neighbour on the nearer side along each axis.
-template <typename T>
-__device__ __forceinline__ bool neighbourhood(const StepParams<T> &p, V3<T> x, int32_t &cx, int32_t &cy, int32_t &cz,
-                                              int32_t &sx, int32_t &sy, int32_t &sz) {
-    if (!cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) return false;
-    sx = (x.x * p.grid.inv_cs - (T)cx < T(0.5)) ? -1 : 1;
-    sy = (x.y * p.grid.inv_cs - (T)cy < T(0.5)) ? -1 : 1;
-    sz = (x.z * p.grid.inv_cs - (T)cz < T(0.5)) ? -1 : 1;
-    return true;
-}
-
-// Insert partner id j into a per-body list kept ascending in LDS.
-template <int MAXP>
-__device__ __forceinline__ void list_insert(int32_t *s_id, int stride, int slot, int32_t &np_, int32_t j,
-                                            bool &overflow) {
-    int pos = np_;
-    while (pos > 0) {
-        const int32_t prev = s_id[(pos - 1) * stride + slot];
-        if (prev == j) return;                       // reached through two hashed cells
-        if (prev < j) break;
-        --pos;
-    }
-    if (np_ >= MAXP) { overflow = true; return; }
-    for (int t = np_; t > pos; --t) s_id[t * stride + slot] = s_id[(t - 1) * stride + slot];
-    s_id[pos * stride + slot] = j;
-    ++np_;
-}
-
-// K1, one lane per body: the 8 bucket counts and the first 4 ids of each
-// bucket are loaded together, then candidates in batches of RB_QBATCH
-// (snapshot loads in flight together).  Returns the partner count.
+// K1, one lane per body (rb_grid.hpp search_buckets with the main law's
+// candidate test).
 template <typename T, int MAXP>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                    T rad, T bi, int32_t *s_id, int tid) {
-    constexpr int NB = STEP_BLOCK;
-    int32_t cx, cy, cz, sx, sy, sz;
-    if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) { atomicOr(p.err, ERR_DOMAIN); return 0; }
-    uint32_t b[8];
-    int32_t c[8];
-    uint4 id4[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid.hmask);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) id4[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H), c[k]);
-    int32_t total = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        int32_t n = c[k];
-#pragma unroll
-        for (int j = 0; j < k; ++j)
-            if (b[j] == b[k]) n = 0;                  // two cells hashed to one bucket: visit once
-        c[k] = n;
-        total += n;
-    }
-    int32_t np_ = 0;
-    bool overflow = false;
-    for (int base = 0; base < total; base += RB_QBATCH) {
-        uint32_t tj[RB_QBATCH];
-        Snap<T> sn[RB_QBATCH];
-#pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) {
-            int32_t rem = base + u;
-            uint32_t t = (uint32_t)i;
-            int64_t addr = -1;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (rem >= 0 && rem < c[k]) {
-                    if (rem == 0) t = id4[k].x;
-                    else if (rem == 1) t = id4[k].y;
-                    else if (rem == 2) t = id4[k].z;
-                    else if (rem == 3) t = id4[k].w;
-                    else addr = (int64_t)b[k] * BUCKET_SLOTS + rem;
-                }
-                rem -= c[k];
-            }
-            if (base + u < total && addr >= 0) t = p.cur.ids[CHK(addr, (int64_t)p.grid.H * BUCKET_SLOTS)];
-            tj[u] = (base + u < total) ? t : (uint32_t)i;
-        }
-        // the id-indexed snapshot: ids are spatially coherent, so a wave's
-        // candidates share lines (cheaper than bucket slots at this scale)
-#pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
-#pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u)
-            if (candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u]))
-                list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
-    }
-    if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
-    return np_;
+    return search_buckets<T, MAXP>(p, i, x, s_id, tid, [&](uint32_t tj, const Snap<T> &s) {
+        return candidate_hit(p, i, kind, x, rad, bi, tj, s);
+    });
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
 // cell k.  Its count, first ids and first RB_QBATCH slot snapshots are
 // loaded together (slots past the count are stale and ignored), and while
 // they are in flight the lane evaluates the body's inverse world inertia
-// (pre, optional).  Hits become a bitmask over the bucket slots; a group prefix sum
+// (pre, if PRE).  Hits become a bitmask over the bucket slots; a group prefix sum
 // (shuffles) places them — id and snapshot — in LDS, and the group
 // rank-sorts them by body id into s_id / s_pos.  Same contact set and order
 // as search_partners.
-template <typename T, int MAXP, int G>
+template <typename T, int MAXP, int G, bool PRE>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
                                                V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
-                                               Snap<T> *t_pos, int slot, int k, int lane, LazyInvI<T> *pre) {
+                                               Snap<T> *t_pos, int slot, int k, int lane, LazyInvI<T> &pre) {
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
     constexpr int QB = RB_QBATCH;
@@ -369,7 +167,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
 #pragma unroll
         for (int u = 0; u < QB; ++u) p4[u] = p.cur.pos[base + u];
     }
-    if (pre) pre->get();                          // overlaps the bucket loads
+    if constexpr (PRE) pre.get();                 // overlaps the bucket loads
     STAMP(9);
     const int gbase = lane & ~(G - 1);
 #pragma unroll
@@ -454,22 +252,16 @@ template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepP
     return b;
 }
 
-// Where body_update finds a body's sorted partner list: ids at id[u *
-// stride] (an LDS column, or the global per-slot list of the split form),
-// snapshots at pos[u * stride] (LDS, cooperative form) or, pos == nullptr,
-// gathered from the step-start snapshot.
-template <typename T> struct Partners {
-    const int32_t *id;
-    int64_t stride;
-    const Snap<T> *pos;
-};
-
 // Everything after the contact search for one body (lane): gravity, the
 // Gauss-Seidel solves in canonical order, integration, next-step insert.
-template <typename T>
+// The sorted partner list: ids at pid[u * stride] (an LDS column, or the
+// split form's per-slot list in HBM); snapshots at ppos[u * stride] (LDS,
+// POS = true: cooperative form) or gathered from the step-start snapshot.
+// POS is a template flag so LDS accesses stay ds_read (no flat loads).
+template <typename T, bool POS>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, LazyInvI<T> &invI, int32_t np_,
-                                            const Partners<T> &P, int tid) {
+                                            const int32_t *pid, int64_t stride, const Snap<T> *ppos, int tid) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -524,10 +316,13 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
         Snap<T> pe[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (s0 + u < np_) jj[u] = P.id[CHK((s0 + u) * P.stride, 32 * P.stride)];
+            if (s0 + u < np_) jj[u] = pid[CHK((s0 + u) * stride, 32 * stride)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (s0 + u < np_) pe[u] = P.pos ? P.pos[(s0 + u) * P.stride] : p.snap_cur[CHK(jj[u], p.n_global)];
+        for (int u = 0; u < 4; ++u) {
+            if (s0 + u >= np_) continue;
+            if constexpr (POS) pe[u] = ppos[(s0 + u) * stride];
+            else pe[u] = p.snap_cur[CHK(jj[u], p.n_global)];
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (s0 + u >= np_) break;
@@ -602,8 +397,8 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
         if (RB_ABLATE != 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid);
     } else {
         if (RB_ABLATE != 1)
-            np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                          &invI);
+            np_ = search_coop<T, MAXP, G, true>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k,
+                                                tid, invI);
     }
     STAMP(2);
     if (!active || k != 0 || RB_ABLATE == 4) return;
@@ -612,12 +407,11 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
         invI.I = in.I;
         invI.q = in.q;
     }
-    const Partners<T> P{s_id + slot, NB, G > 1 ? s_pos + slot : nullptr};
-    body_update<T>(p, l, i, x, kind, sz, bi, in, invI, np_, P, tid);
+    body_update<T, (G > 1)>(p, l, i, x, kind, sz, bi, in, invI, np_, s_id + slot, NB, s_pos + slot, tid);
 }
 
 template <typename T, int MAXP, int G>
-__global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
+__device__ __forceinline__ void step_body(const StepParams<T> &p) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
@@ -637,6 +431,21 @@ __global__ __launch_bounds__(STEP_BLOCK) void step_kernel(StepParams<T> p) {
     // a store waits for it (vmcnt counts in issue order).
     for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
 }
+
+// The two forms as separate kernels: the one-lane (large-scene) form may be
+// compiled for more waves per SIMD — its dependent random loads want
+// occupancy more than registers — without touching the cooperative form.
+#ifndef RB_MIN_WAVES_G1
+#define RB_MIN_WAVES_G1 1
+#endif
+template <typename T, int MAXP>
+__global__ __launch_bounds__(STEP_BLOCK) void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8>(p); }
+template <typename T, int MAXP>
+__global__ __launch_bounds__(STEP_BLOCK)
+#if RB_MIN_WAVES_G1 > 1
+__attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_G1)))
+#endif
+void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1>(p); }
 
 // ---- split form (large scenes): search kernel + update kernel -------------
 // The fused kernel's register footprint (the f64 solve) caps it at two
@@ -663,9 +472,10 @@ __global__ __launch_bounds__(STEP_BLOCK) void search_kernel(StepParams<T> p) {
     const int32_t kind = p.cs.kind[i];
     const T rad = p.cs.sx[i];
     int32_t np_;
+    LazyInvI<T> unused;
     if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, rad, self.r, s_id, tid);
-    else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                       (LazyInvI<T> *)nullptr);
+    else np_ = search_coop<T, MAXP, G, false>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k,
+                                              tid, unused);
     if (!active) return;
     for (int s = k; s < np_; s += G) p.plist[CHK((int64_t)s * p.S + l, (int64_t)MAXP * p.S)] = s_id[s * NB + slot];
     if (k == 0) p.plist_cnt[CHK(l, p.S)] = np_;
@@ -688,8 +498,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
         invI.q = in.q;
         const int32_t np_ = p.plist_cnt[CHK(l, p.S)];
         if (RB_BOUNDS && np_ > 16) printf("RB_BOUNDS np_ %d at l %d\n", np_, l);
-        const Partners<T> P{p.plist + l, p.S, nullptr};
-        body_update<T>(p, l, i, x, kind, sz, self.r, in, invI, np_, P, tid);
+        body_update<T, false>(p, l, i, x, kind, sz, self.r, in, invI, np_, p.plist + l, p.S, nullptr, tid);
     }
     for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
 }
@@ -764,11 +573,11 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, b
         else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     } else if (coop) {
-        if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16, 8>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((step_kernel<T, 32, 8>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     } else {
-        if (maxp <= 16) hipLaunchKernelGGL((step_kernel<T, 16, 1>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((step_kernel<T, 32, 1>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((step_kernel_one<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     }
     return hipGetLastError();
 }

@@ -110,17 +110,23 @@ def _scene_of(model) -> Scene:
     return sc if sc is not None else scene_from_mujoco(model)
 
 
-def world_for(model, normal_convention: str = "oriented") -> World:
+def world_for(model, normal_convention: str = "oriented", law: str = "mujoco", tol: float = 0.01) -> World:
+    """The cached GPU world of `model` (one per model and contact law)."""
     try:
-        w = _worlds.get(model)
+        ws = _worlds.get(model)
     except TypeError:
-        w = _worlds_by_id.get(id(model))
-    if w is None:
-        w = World(_scene_of(model), normal_convention=normal_convention)
+        ws = _worlds_by_id.get(id(model))
+    if ws is None:
+        ws = {}
         try:
-            _worlds[model] = w
+            _worlds[model] = ws
         except TypeError:
-            _worlds_by_id[id(model)] = w
+            _worlds_by_id[id(model)] = ws
+    w = ws.get(law)
+    if w is None:
+        w = ws[law] = World(_scene_of(model), normal_convention=normal_convention, law=law, tol=tol)
+    elif law == "balls" and w.tol != tol:
+        w.set_contact_law(law, tol)
     return w
 
 
@@ -142,9 +148,10 @@ def body_index(model, obj: str) -> int:
 
 
 def step_model(model, data, nsteps: int, dt: float, restitution: float, friction: float,
-               threshold: float, normal_convention: str = "oriented") -> None:
+               threshold: float, normal_convention: str = "oriented", law: str = "mujoco",
+               tol: float = 0.01) -> None:
     """Upload data's state, run nsteps reference steps on the GPU, write back."""
-    w = world_for(model, normal_convention)
+    w = world_for(model, normal_convention, law, tol)
     w.set_state(np.asarray(data.qpos).reshape(-1, 7), np.asarray(data.qvel).reshape(-1, 6))
     xf = np.asarray(getattr(data, "xfrc_applied", np.zeros((1, 6))))
     first = getattr(model, "FIRST", SceneModel.FIRST)

@@ -108,6 +108,42 @@ def multi_sphere4() -> Scene:
                  names=["ball1", "ball2", "ball3", "ball4"])
 
 
+def ball_collision(spin: bool = False) -> Scene:
+    """models/ball_collision.xml + ball_collision.py:31-34 (two balls r 0.1
+    thrown at each other; e 1.0, mu 0.3: sim_overrides.py:16-21; dt 0.01).
+    The two-ball contact law (rbhip.World(..., law="balls")).  spin=True:
+    a y-offset and initial spins, so the friction and torque terms act."""
+    kind, mass, inertia, size = _spheres(2, 0.1, M_SPHERE_R01, I_SPHERE_R01)
+    qpos = np.array([[-1.0, 0.0, 1.0, 1.0, 0.0, 0.0, 0.0], [1.0, 0.0, 1.0, 1.0, 0.0, 0.0, 0.0]])
+    qvel = np.array([[1.0, 0.0, 0.5, 0.0, 0.0, 0.0], [-1.0, 0.0, 0.5, 0.0, 0.0, 0.0]])
+    if spin:
+        qpos[1, 1] = 0.06
+        qvel[0, 3:6] = [0.0, 4.0, 2.0]
+        qvel[1, 3:6] = [1.0, -2.0, 0.0]
+    return Scene("ball_collision", kind, mass, inertia, size, _flat_plane(), qpos, qvel,
+                 dt=0.01, restitution=1.0, friction=0.3, threshold=0.0, names=["ball1", "ball2"])
+
+
+def balls_pile(nx: int, ny: int, seed: int = 0, spacing: float = 0.25) -> Scene:
+    """N-ball generalisation of the two-ball law: an nx*ny grid of r 0.1
+    balls dropped from z ~ U(0.3, 1.5) with v_xy ~ N(0, 1), close enough that
+    neighbours collide; e 0.9, mu 0.3, dt 0.01."""
+    n = nx * ny
+    rng = np.random.default_rng(seed)
+    kind, mass, inertia, size = _spheres(n, 0.1, M_SPHERE_R01, I_SPHERE_R01)
+    iy, ix = np.divmod(np.arange(n), nx)
+    qpos = np.zeros((n, 7))
+    qpos[:, 0] = (ix - (nx - 1) / 2.0) * spacing
+    qpos[:, 1] = (iy - (ny - 1) / 2.0) * spacing
+    qpos[:, 2] = rng.uniform(0.3, 1.5, n)
+    qpos[:, 3] = 1.0
+    qvel = np.zeros((n, 6))
+    qvel[:, 0:2] = rng.normal(0.0, 1.0, (n, 2))
+    qvel[:, 3:6] = rng.normal(0.0, 3.0, (n, 3))
+    return Scene(f"balls_pile_{n}", kind, mass, inertia, size, _flat_plane(), qpos, qvel,
+                 dt=0.01, restitution=0.9, friction=0.3, threshold=0.0)
+
+
 def flat_spheres(nx: int, ny: int, seed: int = 0, spacing: float = 0.3) -> Scene:
     """C2/C3 — nx*ny spheres r 0.1 on flat ground, grid spacing 0.3 (3r),
     z0 ~ U(0.15, 2.0), v_xy ~ N(0, 0.3^2), v_z = 0, w ~ N(0, 2^2);
@@ -193,7 +229,7 @@ def make(name: str, **kw) -> Scene:
     if name in CONFIGS:
         return CONFIGS[name](**kw)
     table = {"single_sphere": single_sphere, "single_cube": single_cube,
-             "multi_sphere": multi_sphere4}
+             "multi_sphere": multi_sphere4, "ball_collision": ball_collision}
     if name in table:
         return table[name]()
     raise KeyError(f"unknown scene {name!r}; known: {sorted(CONFIGS) + sorted(table)}")

@@ -19,7 +19,10 @@ from .scenes import Scene
 class World:
     def __init__(self, scene: Scene, device: int = 0, dtype: str = "f64", rank: int = 0,
                  world_size: int = 1, max_partners: int = 16, bucket_capacity: int = 0,
-                 normal_convention: Optional[str] = None):
+                 normal_convention: Optional[str] = None, law: str = "mujoco", tol: float = 0.01):
+        """law: "mujoco" — the per-body Gauss-Seidel law of collision.py /
+        multi_sphere_bounce.py; "balls" — the two-ball law of
+        ball_collision.py:73-125 (tol: its contact tolerance, :102)."""
         L = _lib.load()
         self.scene = scene
         self.dtype = dtype
@@ -54,7 +57,16 @@ class World:
         S = -(-scene.n // world_size)
         self.lo = S * rank
         self.hi = min(self.lo + S, scene.n)
+        self.law = "mujoco"
+        if law != "mujoco":
+            self.set_contact_law(law, tol)
         self.set_state(scene.qpos0, scene.qvel0)
+
+    def set_contact_law(self, law: str, tol: float = 0.01):
+        """Switch between the default law and the two-ball law (rb_set_contact_law)."""
+        code = {"mujoco": _lib.RB_LAW_MUJOCO, "balls": _lib.RB_LAW_BALLS}[law]
+        _lib.check(self._L.rb_set_contact_law(self._h, code, float(tol)), "rb_set_contact_law")
+        self.law, self.tol = law, float(tol)
 
     # ---- lifetime ---------------------------------------------------------
     def close(self):
@@ -187,4 +199,15 @@ def kat_apply(inp: np.ndarray, dtype: str = "f64", device: int = 0) -> np.ndarra
     out = np.zeros((inp.shape[0], 6))
     _lib.check(L.rb_kat_apply(device, _lib.RB_F64 if dtype == "f64" else _lib.RB_F32, inp.shape[0],
                               _lib.ptr(inp), _lib.ptr(out)), "rb_kat_apply")
+    return out
+
+
+def kat_pair_impulse(inp: np.ndarray, dtype: str = "f64", device: int = 0) -> np.ndarray:
+    """Device known-answer entry: compute_collision_impulse (ball_collision.py:53-68)
+    per row of inp[:, 27] = m, e, mu, v, w, r, n, I_inv(9) -> out[:, 3]."""
+    L = _lib.load()
+    inp = np.ascontiguousarray(inp, np.float64).reshape(-1, 27)
+    out = np.zeros((inp.shape[0], 3))
+    _lib.check(L.rb_kat_pair_impulse(device, _lib.RB_F64 if dtype == "f64" else _lib.RB_F32, inp.shape[0],
+                                     _lib.ptr(inp), _lib.ptr(out)), "rb_kat_pair_impulse")
     return out

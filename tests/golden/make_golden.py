@@ -13,6 +13,9 @@ What is called from the reference (paths relative to its root):
   src/physics/collision.py:51-53    compute_inertia_tensor_world
   src/physics/collision.py:56-102   custom_step_with_impulse_collision_friction (C1)
   src/physics/time_integeration.py:13-72 timestep_integration (single cube)
+  src/simulation/ball_collision.py:39-125 compute_inverse_inertia,
+                                    compute_collision_impulse,
+                                    step_with_custom_collisions (two balls)
 
 MuJoCo is not installed here (and not installable offline), so the module
 `mujoco` those files import is pre-seeded in sys.modules with a stub that
@@ -20,6 +23,13 @@ provides exactly what they call: mj_forward (contact generation, restated
 below in plain Python floats from MuJoCo's published plane-sphere,
 plane-box and sphere-sphere primitives — an independent restatement from
 the C oracle's), mj_name2id, mjtObj and mju_mulQuat.
+
+ball_collision.py cannot be imported either (GLFW window, viewer loop and
+MjModel load at module level); its three functions are extracted with `ast`
+and exec'd with the module globals they read injected (masses and inverse
+inertias computed by the extracted compute_inverse_inertia, the config's
+e 1.0 / mu 0.3: sim_overrides.py:16-21, ball_radius 0.1: :23).  Their
+mj.mj_forward call only refreshes MuJoCo internals the law never reads.
 
 The N-body driver custom_step_multi_sphere (multi_sphere_bounce.py:42-92)
 cannot be imported (module-level GLFW/viewer side effects) and crashes as
@@ -424,6 +434,78 @@ def run_nbody(ref, sc: scenes.Scene, steps: int, every: int, contact_steps: int)
                 c_dist=np.concatenate(c_dist) if c_dist else np.zeros(0))
 
 
+# ----------------------------------------------------------------------------
+# ball_collision.py: the two-ball law
+# ----------------------------------------------------------------------------
+
+BALL_FUNCS = ("compute_inverse_inertia", "compute_collision_impulse", "step_with_custom_collisions")
+
+
+def load_ball_law(reference: str, mass1: float, mass2: float, restitution: float = 1.0,
+                  friction: float = 0.3, radius: float = 0.1):
+    """The three functions of ball_collision.py, exec'd from their own source
+    with the module globals they use."""
+    import ast
+    path = os.path.join(reference, "src", "simulation", "ball_collision.py")
+    tree = ast.parse(open(path).read(), path)
+    defs = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in BALL_FUNCS]
+    assert sorted(d.name for d in defs) == sorted(BALL_FUNCS)
+    mod = ast.Module(body=defs, type_ignores=[])
+    ns = {"np": np, "mj": types.SimpleNamespace(mj_forward=lambda model, data: None),
+          "ball_radius": radius, "restitution": restitution, "friction_coefficient": friction,
+          "mass1": mass1, "mass2": mass2}
+    exec(compile(mod, path, "exec"), ns)
+    ns["I_inv_ball1"] = ns["compute_inverse_inertia"](mass1, radius)
+    ns["I_inv_ball2"] = ns["compute_inverse_inertia"](mass2, radius)
+    return ns
+
+
+def gen_kat_pair_impulse(law, rng, n_random=1500):
+    """compute_collision_impulse(mass, I_inv, v, w, r, n, e, mu) cases:
+    in[27] = m, e, mu, v3, w3, r3, n3, I_inv9 -> out[3]."""
+    rows = []
+    iinv = law["I_inv_ball1"]
+    for k in range(n_random):
+        m = float(rng.uniform(0.05, 5.0))
+        e = float(rng.choice([0.0, 0.2, 0.8, 1.0, rng.uniform(0, 1)]))
+        mu = float(rng.choice([0.0, 0.3, 1.0, rng.uniform(0, 2)]))
+        v, w = rng.normal(0, 2, 3), rng.normal(0, 5, 3)
+        nrm = rng.normal(size=3)
+        nrm /= np.linalg.norm(nrm)
+        r = -0.1 * nrm + rng.normal(0, 0.01, 3) * (k % 3 == 0)
+        I = iinv if k % 2 == 0 else np.linalg.inv(np.diag(rng.uniform(0.1, 2.0, 3)))
+        rows.append((m, e, mu, v, w, r, nrm, I))
+    # edge cases: |v_t| at and around the 1e-8 switch, pure normal motion,
+    # separating contacts (the law applies them anyway), clip on both sides
+    nz = np.array([0.0, 0.0, 1.0])
+    rz = np.array([0.0, 0.0, -0.1])
+    for vt in (0.0, 1e-8, np.nextafter(1e-8, 1), np.nextafter(1e-8, 0), 1e-9, 1e-7):
+        rows.append((0.2, 1.0, 0.3, np.array([vt, 0.0, -1.0]), np.zeros(3), rz, nz, iinv))
+    rows.append((0.2, 1.0, 0.3, np.array([0.0, 0.0, 2.0]), np.zeros(3), rz, nz, iinv))
+    rows.append((0.2, 0.5, 0.01, np.array([3.0, 0.0, -0.1]), np.zeros(3), rz, nz, iinv))
+    rows.append((0.2, 0.5, 5.0, np.array([-3.0, 1.0, -0.1]), np.array([0.0, 9.0, 0.0]), rz, nz, iinv))
+    inp = np.zeros((len(rows), 27))
+    out = np.zeros((len(rows), 3))
+    for k, (m, e, mu, v, w, r, nrm, I) in enumerate(rows):
+        inp[k, 0:3] = m, e, mu
+        inp[k, 3:6], inp[k, 6:9], inp[k, 9:12], inp[k, 12:15] = v, w, r, nrm
+        inp[k, 15:24] = np.asarray(I).reshape(9)
+        out[k] = law["compute_collision_impulse"](m, np.asarray(I), v.copy(), w.copy(), r.copy(), nrm.copy(), e, mu)
+    return inp, out
+
+
+def run_balls(law, qpos0, qvel0, steps: int, dt: float = 0.01):
+    """step_with_custom_collisions on a two-ball data, every step recorded."""
+    model = types.SimpleNamespace(opt=types.SimpleNamespace(gravity=np.array([0.0, 0.0, -9.8])))
+    data = types.SimpleNamespace(qpos=qpos0.reshape(-1).copy(), qvel=qvel0.reshape(-1).copy())
+    qs, vs = [], []
+    for _ in range(steps):
+        law["step_with_custom_collisions"](model, data, dt)
+        qs.append(data.qpos.copy())
+        vs.append(data.qvel.copy())
+    return np.array(qs).reshape(steps, -1, 7), np.array(vs).reshape(steps, -1, 6)
+
+
 def scene_arrays(sc: scenes.Scene):
     return dict(kind=sc.kind, mass=sc.mass, inertia=sc.inertia, size=sc.size, planes=sc.planes,
                 gravity=sc.gravity, qpos0=sc.qpos0, qvel0=sc.qvel0,
@@ -486,6 +568,18 @@ def main():
             res = run_nbody(ref, sc, steps, every, csteps)
             out(name, **res, **scene_arrays(sc))
             print(name, "done", res["c_partner"].shape)
+    # the two-ball law: ball_collision.py:31-34 initial conditions, and a
+    # variant with an offset and spins so friction and torque terms act
+    m = scenes.M_SPHERE_R01
+    law = load_ball_law(args.reference, m, m)
+    if want("kat_pair_impulse"):
+        inp, res = gen_kat_pair_impulse(law, np.random.default_rng(20251015))
+        out("kat_pair_impulse", inp=inp, out=res)
+    for name, sc in (("traj_balls2", scenes.ball_collision()), ("traj_balls2_spin", scenes.ball_collision(spin=True))):
+        if want(name):
+            q, v = run_balls(law, sc.qpos0, sc.qvel0, 600, sc.dt)
+            out(name, qpos=q, qvel=v, tol=np.array(0.01), **scene_arrays(sc))
+            print(name, "done")
 
 
 if __name__ == "__main__":

@@ -128,3 +128,49 @@ def test_oracle_thread_count_invariant(oracle):
         assert np.array_equal(q, q1) and np.array_equal(v, v1)
         for a, b in zip(c, c1):
             assert np.array_equal(a, b)
+
+
+# ---- the two-ball law (ball_collision.py:39-125) ---------------------------
+
+def test_kat_pair_impulse_bit_exact(oracle):
+    """compute_collision_impulse (ball_collision.py:53-68) on 1,509 cases,
+    including |v_t| around the 1e-8 switch and friction clipped both ways."""
+    g = load_golden("kat_pair_impulse")
+    assert np.array_equal(oracle.kat_pair_impulse(g["inp"]), g["out"])
+
+
+@pytest.mark.parametrize("name", ["traj_balls2", "traj_balls2_spin"])
+def test_two_ball_trajectory_bit_exact(oracle, name):
+    """step_with_custom_collisions (ball_collision.py:73-125), 600 steps, every
+    step; the run goes through ground bounces and the ball-ball collision."""
+    g = load_golden(name)
+    sc = golden_scene(g)
+    osc = oracle.OracleScene(sc)
+    q, v = sc.qpos0, sc.qvel0
+    q1, v1 = oracle.pair_step(osc, sc.qpos0, sc.qvel0, 1, tol=float(g["tol"]))
+    assert np.array_equal(q1, g["qpos"][0]) and np.array_equal(v1, g["qvel"][0])
+    for t in range(g["qpos"].shape[0]):
+        q, v = oracle.pair_step(osc, q, v, 1, tol=float(g["tol"]))
+        assert np.array_equal(q, g["qpos"][t]) and np.array_equal(v, g["qvel"][t]), t
+    qn, vn = oracle.pair_step(osc, sc.qpos0, sc.qvel0, g["qpos"].shape[0], tol=float(g["tol"]))
+    assert np.array_equal(qn, g["qpos"][-1]) and np.array_equal(vn, g["qvel"][-1])
+    d = np.linalg.norm(g["qpos"][:, 1, :3] - g["qpos"][:, 0, :3], axis=1)
+    assert d.min() < 0.21 and g["qpos"][:, :, 2].min() < 0.1      # both contact kinds happened
+
+
+def test_ball_law_pile_pairs(oracle):
+    """N-ball generalisation: pairs found are exactly those within r_a + r_b
+    + tol (brute force on the post-ground positions of the last step)."""
+    from rbhip import scenes
+    sc = scenes.balls_pile(8, 8, seed=1)
+    osc = oracle.OracleScene(sc)
+    q, v = oracle.pair_step(osc, sc.qpos0, sc.qvel0, 60)
+    q2, v2, (cnt, par) = oracle.pair_step(osc, q, v, 1, record=True)
+    assert cnt.sum() > 0 and cnt.sum() % 2 == 0
+    # rebuild the post-ground positions and check the pair set
+    p = q[:, :3].copy()
+    p[:, 2] = np.where(p[:, 2] < 0.1, 0.1, p[:, 2])
+    off = np.concatenate([[0], np.cumsum(cnt)])
+    for i in range(sc.n):
+        want = [j for j in range(sc.n) if j != i and np.linalg.norm(p[max(i, j)] - p[min(i, j)]) < 0.21]
+        assert list(par[off[i]:off[i + 1]]) == want
