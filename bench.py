@@ -173,7 +173,9 @@ def main():
                    "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "rb::step_kernel", "avg_launch_ms": avg_ms, "launches_timed": launches,
+                     "kernel": ("rb::step_kernel_coop" if w.n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "32768"))
+                                else "rb::step_kernel_one"),
+                     "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
