@@ -103,3 +103,32 @@ def test_single_body_entry_rejects_multi_body_scene():
     g, sc, model, data = _model_data("traj_multi4")
     with pytest.raises(ValueError, match="several free bodies"):
         timestep_integration(model, "ball1", data)
+
+
+# ---- the headless runner (src/simulate.py) ---------------------------------
+@pytest.mark.parametrize("sim,golden,steps", [("single_sphere", "traj_single_sphere", 300),
+                                              ("cube_incline", "traj_single_cube", 300),
+                                              ("ball_collision", "traj_balls2", 300)])
+def test_simulate_runs_match_reference(sim, golden, steps, tmp_path):
+    from src import simulate
+    g = load_golden(golden)
+    q, v, logger = simulate.run(sim, steps, log_every=10, out=str(tmp_path))
+    # single-body goldens hold the initial state at row 0; the two-ball one starts after step 1
+    gq, gv = (g["qpos"][steps][None], g["qvel"][steps][None]) if g["qpos"].ndim == 2 else \
+        (g["qpos"][steps - 1], g["qvel"][steps - 1])
+    assert np.array_equal(q, gq) and np.array_equal(v, gv)
+    traj = np.load(tmp_path / f"{sim}_trajectory.npz")
+    assert len(traj.files) >= 1
+    if sim != "ball_collision":
+        t = traj["trajectory"]
+        assert t.shape == (steps // 10, 4) and np.array_equal(t[-1, 1:], gq[0, :3])
+
+
+def test_simulate_multi_sphere_vs_oracle(oracle):
+    from src import simulate
+    from rbhip import scenes
+    sc = scenes.multi_sphere4()
+    qo, vo = oracle.step(oracle.OracleScene(sc), sc.qpos0, sc.qvel0, 250)
+    q, v, logger = simulate.run("multi_sphere", 250, log_every=50)
+    assert np.array_equal(q, qo) and np.array_equal(v, vo)
+    assert len(logger.loggers["ball1"].times) == 5
