@@ -486,8 +486,13 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxp = maxp;
     w->maxrec = 4 * w->n_planes + w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
-    // per-cell hash: >= 4 buckets per body (occupied cells <= bodies)
-    w->H = next_pow2(4 * w->N > 4096 ? 4 * w->N : 4096);
+    // per-cell hash: 16 buckets per body (occupied cells <= bodies), so few
+    // cells share a bucket and few false candidates are read (measured: C3
+    // +15% over 4 per body); at most 2^26 buckets (8 GB of id lines)
+    int64_t hfac = 16;
+    if (const char *ev = getenv("RBHIP_HASH_FACTOR")) hfac = atoll(ev) > 0 ? atoll(ev) : 16;
+    int64_t want = hfac * w->N > 4096 ? hfac * w->N : 4096;
+    w->H = next_pow2(want < (int64_t(1) << 26) ? want : (int64_t(1) << 26));
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
     // algorithmic bytes per body-step: 13 state reals read + 13
