@@ -79,9 +79,18 @@ __device__ __forceinline__ void ball_ground(const StepParams<T> &p, V3<T> &x, V3
 }
 
 // |p_b - p_a| < r_a + r_b + tol for the pair (a < b), ball_collision.py:100-103
+// (decided on the squared distance when clear of the threshold, see
+// sphere_sphere_hit)
 template <typename T> __device__ __forceinline__ bool ball_hit(V3<T> pa, T ra, V3<T> pb, T rb, T tol) {
     const V3<T> d = {pb.x - pa.x, pb.y - pa.y, pb.z - pa.z};
-    return sqroot(np_dot(d, d)) < (ra + rb) + tol;
+    const T d2 = np_dot(d, d);
+    const T L = (ra + rb) + tol;
+    const T L2 = L * L;
+    if (RB_SQ_PREFILTER) {
+        if (d2 > L2 * (T(1) + sq_margin<T>())) return false;
+        if (d2 < L2 * (T(1) - sq_margin<T>())) return true;
+    }
+    return sqroot(d2) < L;
 }
 
 template <typename T, int MAXP>

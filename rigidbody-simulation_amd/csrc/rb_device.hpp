@@ -240,11 +240,28 @@ __device__ __forceinline__ bool plane_box_corner(V3<T> pn, V3<T> c, T dist, cons
     return true;
 }
 
-// mjc_SphereSphere, geom1 = lower body id; test-only variant first
+// Relative margin under which a squared-distance comparison decides a
+// distance test without the square root: far above the rounding of d^2 and
+// R^2 (a few ulp), so the decision equals the exact sqrt(d^2) vs R one.
+#ifndef RB_SQ_PREFILTER
+#define RB_SQ_PREFILTER 1
+#endif
+template <typename T> __device__ __forceinline__ T sq_margin() { return sizeof(T) == 8 ? T(1e-9) : T(1e-4); }
+
+// mjc_SphereSphere, geom1 = lower body id; test-only variant first.  Most
+// candidates are clearly apart (or clearly overlapping): decided on d^2;
+// the rest (and NaN) by the reference's sqrt comparison.
 template <typename T>
 __device__ __forceinline__ bool sphere_sphere_hit(V3<T> c1, T r1, V3<T> c2, T r2) {
     const V3<T> dif = {c1.x - c2.x, c1.y - c2.y, c1.z - c2.z};
-    return !(sqroot(mj_dot(dif, dif)) > (T(0) + r1) + r2);
+    const T d2 = mj_dot(dif, dif);
+    const T R = (T(0) + r1) + r2;
+    const T R2 = R * R;
+    if (RB_SQ_PREFILTER) {
+        if (d2 > R2 * (T(1) + sq_margin<T>())) return false;
+        if (d2 < R2 * (T(1) - sq_margin<T>())) return true;
+    }
+    return !(sqroot(d2) > R);
 }
 template <typename T>
 __device__ __forceinline__ bool sphere_sphere(V3<T> c1, T r1, V3<T> c2, T r2, Contact<T>& con) {
