@@ -24,6 +24,11 @@
 #ifndef RB_QBATCH
 #define RB_QBATCH 4
 #endif
+// cooperative search: bucket slot snapshots loaded with the bucket head,
+// before its count is known (most buckets hold one or two bodies)
+#ifndef RB_QSPEC
+#define RB_QSPEC 2
+#endif
 
 namespace rb {
 

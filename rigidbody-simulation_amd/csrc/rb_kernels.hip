@@ -134,7 +134,7 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
-// cell k.  Its count, first ids and first RB_QBATCH slot snapshots are
+// cell k.  Its count, first ids and first RB_QSPEC slot snapshots are
 // loaded together (slots past the count are stale and ignored), and while
 // they are in flight the lane evaluates the body's inverse world inertia
 // (pre, if PRE).  Hits become a bitmask over the bucket slots; a group prefix sum
@@ -148,6 +148,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
     constexpr int QB = RB_QBATCH;
+    constexpr int QS = RB_QSPEC;                 // slots loaded before the count is known
     int32_t cx = 0, cy = 0, cz = 0, sx = 1, sy = 1, sz = 1;
     bool ok = active;
     if (active && !neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) {
@@ -161,11 +162,11 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     STAMP(8);
     int32_t c = 0;
     uint4 id4 = {0, 0, 0, 0};
-    Snap<T> p4[QB];
+    Snap<T> p4[QS];
     if (ok) {
         id4 = bucket_head(p.cur, b, c);
 #pragma unroll
-        for (int u = 0; u < QB; ++u) p4[u] = p.cur.pos[base + u];
+        for (int u = 0; u < QS; ++u) p4[u] = p.cur.pos[base + u];
     }
     if constexpr (PRE) pre.get();                 // overlaps the bucket loads
     STAMP(9);
@@ -177,14 +178,15 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     }
     uint32_t mask = 0;
 #pragma unroll
-    for (int u = 0; u < QB; ++u)
+    for (int u = 0; u < QS; ++u)
         if (u < c && candidate_hit(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u])) mask |= 1u << u;
-    for (int s0 = QB; s0 < c; s0 += QB) {
+    for (int s0 = QS; s0 < c; s0 += QB) {
         uint32_t tj[QB];
         Snap<T> sn[QB];
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
-            tj[u] = p.cur.ids[base + s0 + u];
+            if (s0 + u >= c) break;                   // stay inside this bucket's slots
+            tj[u] = bucket_id(p.cur, b, id4, s0 + u);
             sn[u] = p.cur.pos[base + s0 + u];
         }
 #pragma unroll
@@ -203,7 +205,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     if (total > MAXP && k == 0) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
     int o = pre_n;
 #pragma unroll
-    for (int u = 0; u < QB; ++u) {
+    for (int u = 0; u < QS; ++u) {
         if (!((mask >> u) & 1u)) continue;
         if (o < MAXP) {
             t_id[slot * MAXP + o] = (int32_t)bucket_id(p.cur, b, id4, u);
@@ -211,10 +213,10 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         }
         ++o;
     }
-    for (uint32_t rest = mask & ~((1u << QB) - 1u); rest; rest &= rest - 1) {
+    for (uint32_t rest = mask & ~((1u << QS) - 1u); rest; rest &= rest - 1) {
         const int sl = __builtin_ctz(rest);
         if (o < MAXP) {                               // re-read: L1-hot from the batch above
-            t_id[slot * MAXP + o] = (int32_t)p.cur.ids[base + sl];
+            t_id[slot * MAXP + o] = (int32_t)bucket_id(p.cur, b, id4, sl);
             t_pos[slot * MAXP + o] = p.cur.pos[base + sl];
         }
         ++o;
