@@ -447,9 +447,7 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
 #endif
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
-#if RB_MIN_WAVES_COOP > 1
-__attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_COOP)))
-#endif
+__attribute__((amdgpu_waves_per_eu(MAXP <= 16 ? RB_MIN_WAVES_COOP : 2)))   // 32 partners: 2 fit
 void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8>(p); }
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)

@@ -91,3 +91,16 @@ def test_world_requires_library_loudly(tmp_path):
         finally:
             _lib._lib = saved
     assert np is not None
+
+
+def test_kernels_do_not_spill():
+    """Every kernel of librbhip.so compiles for gfx950 with no scratch (a
+    spill or an address-taken local in the step kernels costs latency on
+    every step)."""
+    out = subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc"), "resource-usage"],
+                         capture_output=True, text=True, check=True).stdout
+    names = re.findall(r"Function Name: (\S+)", out)
+    scratch = [int(v) for v in re.findall(r"ScratchSize \[bytes/lane\]: (\d+)", out)]
+    assert names and len(names) == len(scratch)
+    spilled = [n for n, s in zip(names, scratch) if s]
+    assert not spilled, f"kernels with scratch: {spilled}"
