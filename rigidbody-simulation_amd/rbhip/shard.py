@@ -85,16 +85,21 @@ class ShardedWorld:
             self.world.set_stream(self.stream.cuda_stream)
 
     def _buffer(self):
+        """(whole buffer, this rank's slice) of the pending exchange; the two
+        alternating buffers' views are built once."""
         if hasattr(self.world, "exchange_buffer"):
-            return self.world.exchange_buffer(self.torch)
+            buf, n = self.world.exchange_buffer(self.torch)
+            return buf, buf[self.rank * n:(self.rank + 1) * n]
         ptr = self.world.gpos_buffer()[0]
-        if ptr not in self._views:                 # two buffers alternate
-            self._views[ptr] = wrap_gpos(self.world, self.torch)
-        return self._views[ptr]
+        v = self._views.get(ptr)
+        if v is None:
+            buf, n = wrap_gpos(self.world, self.torch)
+            v = self._views[ptr] = (buf, buf[self.rank * n:(self.rank + 1) * n])
+        return v
 
     def _exchange(self):
-        buf, n = self._buffer()
-        mine = buf[self.rank * n:(self.rank + 1) * n]
+        buf, mine = self._buffer()
+        n = mine.numel()
         if self.transport == "nccl":
             # in place: the input is this rank's chunk of the output buffer
             self.dist.all_gather_into_tensor(buf, mine, group=self.group)
