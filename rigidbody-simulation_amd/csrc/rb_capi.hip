@@ -125,6 +125,7 @@ template <typename T> Grid<T> make_grid(const rb_world *w) {
     g.inv_cs = (T)w->inv_cs;
     g.hmask = (uint32_t)(w->H - 1);
     g.H = (int32_t)w->H;
+    g.super = w->N > 300000;
     return g;
 }
 

@@ -156,7 +156,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         ok = false;
     }
     const uint32_t b = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0),
-                                 p.grid.hmask);
+                                 p.grid);
     const int64_t base = (int64_t)b * BUCKET_SLOTS;
     [[maybe_unused]] const int tid = lane;   // STAMP
     STAMP(8);

@@ -118,6 +118,33 @@ def test_c3_one_step_parity_from_evolved_state(rb, oracle):
     assert np.array_equal(gq, q1) and np.array_equal(gv, v1)
 
 
+def test_large_scene_steps_parity(rb, oracle):
+    """409,600 spheres (above 300k the broadphase groups buckets by 2x2x2
+    super-cell): 70 GPU steps, then one recorded step, vs the oracle (16
+    threads) — contacts and state bit-exact."""
+    from rbhip import scenes
+    # grid spacing 0.19 < 2r: neighbours collide once they land
+    sc = scenes.flat_spheres(640, 640, seed=5, spacing=0.19)
+    osc = oracle.OracleScene(sc)
+    oracle.set_threads(16)
+    try:
+        q, v = oracle.step(osc, sc.qpos0, sc.qvel0, 70)
+        q1, v1, (cnt, par, kin, dis) = oracle.step(osc, q, v, 1, record=True)
+    finally:
+        oracle.set_threads(1)
+    with rb.World(sc) as w:
+        w.step(70)
+        gq, gv = w.get_state()
+        assert np.array_equal(gq, q) and np.array_equal(gv, v)
+        w.record_contacts(True)
+        w.step(1)
+        gq, gv = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert np.array_equal(gq, q1) and np.array_equal(gv, v1)
+    assert (kin == 16).sum() > 1000
+
+
 def test_f32_bit_exact_vs_f32_restatement(rb, oracle):
     from rbhip import scenes
     sc = scenes.make("c2")
