@@ -59,12 +59,16 @@ def main():
     data[f"{cfg}_{dtype}"] = {
         "fetch_size_kb_per_launch": f, "write_size_kb_per_launch": w,
         "hbm_bytes_per_launch": guide,
+        "hbm_bytes_per_launch_lower": f * 1024.0 + w * 1024.0,
         "hbm_bytes_per_launch_calibrated": calibrated,
         "correction": "guide: FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950 half-count of wide reads); "
                       "calibrated: factors from profiles/calib_fetch.hip (8 B/lane SoA, known bytes)",
         "calibration": {"known_bytes": known, "fetch_kb": cf, "write_kb": cw,
                         "read_factor": read_factor, "write_factor": write_factor},
-        "note": "FETCH_SIZE counts requests leaving L2, Infinity-Cache (MALL) hits included",
+        "note": "FETCH_SIZE counts requests leaving L2, Infinity-Cache (MALL) hits included; the x2 "
+                "read correction holds for 128-B streaming requests (the state arrays), random 64-B "
+                "gathers (buckets, candidate snapshots) count once: the true figure lies between "
+                "hbm_bytes_per_launch_lower and hbm_bytes_per_launch",
     }
     json.dump(data, open(path, "w"), indent=1)
     print(json.dumps(data[f"{cfg}_{dtype}"], indent=1))
