@@ -100,7 +100,7 @@ __device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int
     const Vel<T> ov = p.vel_cur[i];
     const V3<T> xo = {own.x, own.y, own.z};
     const V3<T> vo = {ov.vx, ov.vy, ov.vz}, wo = {ov.wx, ov.wy, ov.wz};
-    const T mi = p.cs.mass[i], ri = own.r;
+    const T mi = p.cs.mass()[i], ri = own.r;
     const M3<T> Ii = ball_iinv(mi, ri);
 
     // pairs: every partner within reach on the post-ground positions
@@ -120,7 +120,7 @@ __device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int
         const Snap<T> sj = p.snap_cur[j];
         const Vel<T> vj = p.vel_cur[j];
         const V3<T> xj = {sj.x, sj.y, sj.z};
-        const T mj = p.cs.mass[j];
+        const T mj = p.cs.mass()[j];
         const bool self_a = i < j;
         const V3<T> pa = self_a ? xo : xj, pb = self_a ? xj : xo;
         const V3<T> va = self_a ? vo : V3<T>{vj.vx, vj.vy, vj.vz};
@@ -161,9 +161,9 @@ __device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int
 
     // integrate (:121-122): the true end-of-step state
     x = {x.x + v.x * p.dt, x.y + v.y * p.dt, x.z + v.z * p.dt};
-    wt_store(p.st.px + l, x.x); wt_store(p.st.py + l, x.y); wt_store(p.st.pz + l, x.z);
-    wt_store(p.st.vx + l, v.x); wt_store(p.st.vy + l, v.y); wt_store(p.st.vz + l, v.z);
-    wt_store(p.st.wx + l, w.x); wt_store(p.st.wy + l, w.y); wt_store(p.st.wz + l, w.z);
+    wt_store(p.st.px() + l, x.x); wt_store(p.st.py() + l, x.y); wt_store(p.st.pz() + l, x.z);
+    wt_store(p.st.vx() + l, v.x); wt_store(p.st.vy() + l, v.y); wt_store(p.st.vz() + l, v.z);
+    wt_store(p.st.wx() + l, w.x); wt_store(p.st.wy() + l, w.y); wt_store(p.st.wz() + l, w.z);
 
     // the next step's ground phase, then its snapshot and broadphase slot
     ball_ground(p, x, v, w, mi, ri, Ii);
@@ -195,10 +195,10 @@ __global__ __launch_bounds__(256) void ball_prime_kernel(StepParams<T> p) {
     const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= p.n_local) return;
     const int32_t i = p.lo + (int32_t)l;
-    V3<T> x = {p.st.px[l], p.st.py[l], p.st.pz[l]};
-    V3<T> v = {p.st.vx[l], p.st.vy[l], p.st.vz[l]};
-    V3<T> w = {p.st.wx[l], p.st.wy[l], p.st.wz[l]};
-    const T m = p.cs.mass[i], r = p.cs.sx[i];
+    V3<T> x = {p.st.px()[l], p.st.py()[l], p.st.pz()[l]};
+    V3<T> v = {p.st.vx()[l], p.st.vy()[l], p.st.vz()[l]};
+    V3<T> w = {p.st.wx()[l], p.st.wy()[l], p.st.wz()[l]};
+    const T m = p.cs.mass()[i], r = p.cs.sx()[i];
     ball_ground(p, x, v, w, m, r, ball_iinv(m, r));
     Snap<T> sn;
     sn.x = x.x; sn.y = x.y; sn.z = x.z; sn.r = r;
@@ -224,7 +224,7 @@ __global__ void kat_pair_impulse_kernel(int64_t n, const double *in, double *out
 }
 
 template <typename T> hipError_t launch_ball_step(const StepParams<T> &p, int maxp, hipStream_t s) {
-    if (!p.vel_cur || !p.vel_next || !p.st.px) return hipErrorInvalidValue;
+    if (!p.vel_cur || !p.vel_next || !p.st.px()) return hipErrorInvalidValue;
     int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
     if (blocks < 1) blocks = 1;
     if (maxp <= 16) hipLaunchKernelGGL((ball_step_kernel<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
@@ -233,7 +233,7 @@ template <typename T> hipError_t launch_ball_step(const StepParams<T> &p, int ma
 }
 
 template <typename T> hipError_t launch_ball_prime(const StepParams<T> &p, hipStream_t s) {
-    if (!p.vel_next || !p.st.px) return hipErrorInvalidValue;
+    if (!p.vel_next || !p.st.px()) return hipErrorInvalidValue;
     if (p.n_local <= 0) return hipSuccess;
     hipLaunchKernelGGL((ball_prime_kernel<T>), dim3((unsigned)((p.n_local + 255) / 256)), dim3(256), 0, s, p);
     return hipGetLastError();

@@ -142,14 +142,10 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.n_local = w->n_local;
     p.lo = (int32_t)w->lo;
     p.S = (int32_t)w->S;
-    T *st = dp<T>(w->state, 0);
-    T **f[13] = {&p.st.qw, &p.st.qx, &p.st.qy, &p.st.qz, &p.st.vx, &p.st.vy, &p.st.vz, &p.st.wx, &p.st.wy, &p.st.wz,
-                 &p.st.px, &p.st.py, &p.st.pz};
-    for (int k = 0; k < 13; ++k) *f[k] = st + k * w->S;
-    const T *cst = dp<T>(w->consts, 0);
-    p.cs.mass = cst; p.cs.ix = cst + w->Npad; p.cs.iy = cst + 2 * w->Npad; p.cs.iz = cst + 3 * w->Npad;
-    p.cs.sx = cst + 4 * w->Npad; p.cs.sy = cst + 5 * w->Npad; p.cs.sz = cst + 6 * w->Npad;
-    p.cs.bound = cst + 7 * w->Npad;
+    p.st.base = dp<T>(w->state, 0);
+    p.st.S = w->S;
+    p.cs.base = dp<T>(w->consts, 0);
+    p.cs.Npad = w->Npad;
     p.cs.kind = w->kind;
     p.xfrc = w->xfrc ? dp<T>(w->xfrc, 0) : nullptr;
     p.n_planes = w->n_planes;

@@ -209,7 +209,12 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     }
     int32_t np_ = 0;
     bool overflow = false;
-    for (int base = 0; base < total; base += RB_QBATCH) {
+    // at least one batch, even for total == 0 (its candidates are then this
+    // body itself, which hit() rejects): the head loads are used on every
+    // path, so the compiler cannot sink them under a total > 0 branch, behind
+    // the wait for the counts (one dependent round trip more per body)
+    int base = 0;
+    do {
         uint32_t tj[RB_QBATCH];
         Snap<T> sn[RB_QBATCH];
 #pragma unroll
@@ -239,7 +244,8 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
         for (int u = 0; u < RB_QBATCH; ++u)
             if (hit(tj[u], sn[u]))
                 list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
-    }
+        base += RB_QBATCH;
+    } while (base < total);
     if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
     return np_;
 }

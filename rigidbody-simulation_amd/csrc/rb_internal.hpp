@@ -2,6 +2,8 @@
 // C-ABI implementation (rb_capi.hip).  Not part of the public interface.
 #pragma once
 
+#include <cstddef>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,10 +46,22 @@ constexpr int MAX_PLANES = 8;
 // snapshots, except under the two-ball law, whose snapshots hold the next
 // step's post-ground positions: its true positions are px, py, pz.
 template <typename T> struct BodyState {
-    T *qw, *qx, *qy, *qz;
-    T *vx, *vy, *vz;
-    T *wx, *wy, *wz;
-    T *px, *py, *pz;
+    T *base;                           // 13 rows of S reals: qw qx qy qz vx vy vz wx wy wz px py pz
+    int64_t S;
+    __host__ __device__ T *row(int k) const { return base + k * S; }
+    __host__ __device__ T *qw() const { return row(0); }
+    __host__ __device__ T *qx() const { return row(1); }
+    __host__ __device__ T *qy() const { return row(2); }
+    __host__ __device__ T *qz() const { return row(3); }
+    __host__ __device__ T *vx() const { return row(4); }
+    __host__ __device__ T *vy() const { return row(5); }
+    __host__ __device__ T *vz() const { return row(6); }
+    __host__ __device__ T *wx() const { return row(7); }
+    __host__ __device__ T *wy() const { return row(8); }
+    __host__ __device__ T *wz() const { return row(9); }
+    __host__ __device__ T *px() const { return row(10); }
+    __host__ __device__ T *py() const { return row(11); }
+    __host__ __device__ T *pz() const { return row(12); }
 };
 
 // Two-ball law: a ball's post-ground velocity and spin, indexed by global id
@@ -56,10 +70,18 @@ template <typename T> struct alignas(8 * sizeof(T)) Vel { T vx, vy, vz, wx, wy, 
 
 // Per-body constants, global body index (replicated on every rank).
 template <typename T> struct BodyConsts {
-    const T *mass, *ix, *iy, *iz;      // principal inertia (body frame)
-    const T *sx, *sy, *sz;             // sphere radius / box half extents
-    const T *bound;                    // bounding-sphere radius
+    const T *base;                     // 8 rows of Npad reals: mass ix iy iz sx sy sz bound
+    int64_t Npad;
     const int32_t *kind;
+    __host__ __device__ const T *row(int k) const { return base + k * Npad; }
+    __host__ __device__ const T *mass() const { return row(0); }
+    __host__ __device__ const T *ix() const { return row(1); }      // principal inertia (body frame)
+    __host__ __device__ const T *iy() const { return row(2); }
+    __host__ __device__ const T *iz() const { return row(3); }
+    __host__ __device__ const T *sx() const { return row(4); }      // sphere radius / box half extents
+    __host__ __device__ const T *sy() const { return row(5); }
+    __host__ __device__ const T *sz() const { return row(6); }
+    __host__ __device__ const T *bound() const { return row(7); }   // bounding-sphere radius
 };
 
 template <typename T> struct Grid {
@@ -70,10 +92,13 @@ template <typename T> struct Grid {
 };
 
 template <typename T> struct StepParams {
-    int64_t n_global;
-    int32_t n_local, lo;
+    // the first 64 bytes hold everything the step's first loads need, so the
+    // prologue fetches them with one scalar load
+    const Snap<T> *snap_cur;           // step-start snapshot (read)
     BodyState<T> st;
     BodyConsts<T> cs;
+    int32_t n_local, lo;
+    int64_t n_global;
     const T *xfrc;                     // [6][S] or nullptr
     int32_t S;
     int32_t n_planes;
@@ -82,7 +107,6 @@ template <typename T> struct StepParams {
     T dt, e, mu, thr;
     int32_t oriented;
     Grid<T> grid;
-    const Snap<T> *snap_cur;           // step-start snapshot (read)
     Snap<T> *snap_next;                // next step's snapshot (own rows written)
     Table<T> cur;                      // broadphase of snap_cur
     Table<T> next;                     // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
@@ -100,6 +124,9 @@ template <typename T> struct StepParams {
     T *rec_dist;
     int32_t maxrec;
 };
+
+static_assert(offsetof(StepParams<double>, xfrc) == 64 && offsetof(StepParams<float>, xfrc) == 64,
+              "prologue fields must fill the first 64 bytes");
 
 template <typename T> struct InsertParams {
     const Snap<T> *snap;               // [Npad]
