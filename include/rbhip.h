@@ -153,6 +153,25 @@ int rb_shard_exchange_done(rb_world *w);
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems,
                    int32_t *elem_bytes);
 
+/* In-library exchange: the library owns an RCCL communicator over the
+ * world's ranks (RCCL is loaded at first use; the single-GPU path never
+ * needs it) and runs the per-step exchange itself, so K sharded steps --
+ * step kernel, in-place all-gather of the position buffer over xGMI, remote
+ * insert -- replay from one captured HIP graph with no host work per step.
+ * Replaces the per-frame loop of custom_step_multi_sphere
+ * (multi_sphere_bounce.py:42-92) on a body-range sharded scene.
+ *   rb_comm_unique_id: rank 0 creates the communicator id (bytes >= 128)
+ *     and hands it to every rank (e.g. torch.distributed broadcast);
+ *   rb_shard_comm_init: every rank joins (blocks until all have); the
+ *     world's device, rank and world_size define the communicator;
+ *   rb_shard_run: nsteps sharded steps, enqueued only; every rank must make
+ *     the same calls with the same nsteps.  Bit-identical to rb_shard_step +
+ *     all-gather + rb_shard_exchange_done, and to rb_step for world_size 1. */
+int rb_comm_unique_id(void *id, int32_t bytes);
+int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes);
+int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double restitution,
+                 double friction, double contact_threshold);
+
 /* ---- the two-ball law -------------------------------------------------- */
 /* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
  * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;

@@ -7,7 +7,9 @@
 // buffers are fixed by the step counter modulo 6 (tables mod 3, snapshots
 // mod 2), so multi-step calls on a single shard are captured once per
 // phase into a hipGraph (one kernel node per step) and replayed.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: RCCL is dlopen'ed by the sharded path
 
 #include <math.h>
 #include <stdarg.h>
@@ -97,6 +99,7 @@ struct rb_world {
     int32_t *plist_cnt = nullptr;  // split form: [S] partner counts
     int32_t *err = nullptr;
     int32_t *err_host = nullptr;   // pinned
+    ncclComm_t comm = nullptr;     // rb_shard_comm_init: the in-library exchange
     // recording
     bool record = false;
     int32_t *rec_count = nullptr, *rec_partner = nullptr, *rec_kind = nullptr;
@@ -274,14 +277,67 @@ int timed_launch(rb_world *w, double dt, double e, double mu, double thr) {
     return RB_OK;
 }
 
+// RCCL, loaded at first use: only the in-library exchange of sharded worlds
+// needs it (and in a torch process the already-loaded copy is reused)
+struct Rccl {
+    bool tried = false, ok = false;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+Rccl &rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return r;
+    r.GetUniqueId = (decltype(r.GetUniqueId))dlsym(h, "ncclGetUniqueId");
+    r.CommInitRank = (decltype(r.CommInitRank))dlsym(h, "ncclCommInitRank");
+    r.AllGather = (decltype(r.AllGather))dlsym(h, "ncclAllGather");
+    r.CommDestroy = (decltype(r.CommDestroy))dlsym(h, "ncclCommDestroy");
+    r.GetErrorString = (decltype(r.GetErrorString))dlsym(h, "ncclGetErrorString");
+    r.ok = r.GetUniqueId && r.CommInitRank && r.AllGather && r.CommDestroy && r.GetErrorString;
+    return r;
+}
+
+// The in-library exchange after the step kernel of step c (which put the own
+// bodies' new positions in this rank's slice of the next snapshot): the
+// in-place all-gather of that snapshot, then the insert of every other
+// rank's bodies into the next table (as rb_shard_exchange_done).
+int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
+    const int nsp = 1 - (int)(c % 2), nph = (int)((c + 1) % 3);
+    char *buf = static_cast<char *>(w->snap[nsp]);
+    const size_t n = (size_t)4 * w->S;
+    const ncclResult_t r = rccl().AllGather(buf + (size_t)w->esz * n * w->rank, buf, n,
+                                            w->dtype == RB_F64 ? ncclFloat64 : ncclFloat32, w->comm, s);
+    if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
+    const hipError_t ie =
+        w->dtype == RB_F64
+            ? launch_insert<double>(make_insert<double>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), s)
+            : launch_insert<float>(make_insert<float>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), s);
+    HIPCHK(ie);
+    return RB_OK;
+}
+// one sharded step: step kernel, then the exchange
+int shard_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, double mu, double thr) {
+    const int rc = launch_one(w, s, c, dt, e, mu, thr);
+    return rc ? rc : shard_exchange(w, s, c);
+}
+
 void drop_graphs(rb_world *w) {
     for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
     w->graphs.clear();
 }
 
-int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+// nsteps steps (sharded: with the in-library exchange), graph-replayed
+int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
-    if (w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_step + exchange");
+    if (!sharded && w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_run or rb_shard_step + exchange");
+    if (sharded && !w->comm) return fail(RB_EINVAL, "rb_shard_run before rb_shard_comm_init");
+    if (sharded && w->law != RB_LAW_MUJOCO) return fail(RB_EUNSUPPORTED, "sharded stepping supports the default contact law only");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0))
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
@@ -290,27 +346,32 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         int rc = prime(w, dt, e, mu);
         if (rc) return rc;
     }
+    auto one = [&](hipStream_t s, int64_t c) {
+        return sharded ? shard_one(w, s, c, dt, e, mu, thr) : launch_one(w, s, c, dt, e, mu, thr);
+    };
     if (w->timing) {
-        // eager launches, each bracketed by events on the launch stream
+        // eager launches, each step kernel bracketed by events on the launch stream
         for (int64_t k = 0; k < nsteps; ++k) {
             int rc = timed_launch(w, dt, e, mu, thr);
+            if (!rc && sharded) rc = shard_exchange(w, w->stream, w->c);
             if (rc) return rc;
             ++w->c;
         }
         return RB_OK;
     }
     if (nsteps == 1) {
-        int rc = launch_one(w, w->stream, w->c, dt, e, mu, thr);
+        int rc = one(w->stream, w->c);
         if (rc) return rc;
         ++w->c;
         return RB_OK;
     }
+    const int variant = (int)w->record | (sharded ? 2 : 0);
     // K > 1: replay a captured graph of K step nodes
     const int64_t chunk_max = 512;
     int64_t left = nsteps;
     while (left > 0) {
         const int64_t K = left > chunk_max ? chunk_max : left;
-        auto key = std::make_tuple(K, (int)(w->c % 6), dt, e, mu, thr, (int)w->record);
+        auto key = std::make_tuple(K, (int)(w->c % 6), dt, e, mu, thr, variant);
         auto it = w->graphs.find(key);
         if (it == w->graphs.end()) {
             if (w->graphs.size() >= 60) drop_graphs(w);
@@ -321,13 +382,13 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
                 hipGraphExec_t ex;
                 HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
                 for (int64_t k = 0; k < K; ++k) {
-                    int rc = launch_one(w, w->cap_stream, c0 + k, dt, e, mu, thr);
+                    int rc = one(w->cap_stream, c0 + k);
                     if (rc) { (void)hipStreamEndCapture(w->cap_stream, &graph); return rc; }
                 }
                 HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
                 HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
                 (void)hipGraphDestroy(graph);
-                w->graphs[std::make_tuple(K, c0, dt, e, mu, thr, (int)w->record)] = ex;
+                w->graphs[std::make_tuple(K, c0, dt, e, mu, thr, variant)] = ex;
             }
             it = w->graphs.find(key);
         }
@@ -418,6 +479,7 @@ void free_world(rb_world *w) {
     if (!w) return;
     (void)hipSetDevice(w->device);
     drop_graphs(w);
+    if (w->comm) (void)rccl().CommDestroy(w->comm);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
                     w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
@@ -638,6 +700,42 @@ int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *e
     if (shard_elems) *shard_elems = 4 * w->S;
     if (elem_bytes) *elem_bytes = w->esz;
     return RB_OK;
+}
+
+int rb_comm_unique_id(void *id, int32_t bytes) {
+    if (!id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
+    if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
+    ncclUniqueId u;
+    const ncclResult_t r = rccl().GetUniqueId(&u);
+    if (r != ncclSuccess) return fail(RB_ENODEV, "ncclGetUniqueId: %s", rccl().GetErrorString(r));
+    memcpy(id, &u, sizeof(u));
+    return RB_OK;
+}
+
+int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
+    if (!w || !id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "null world or short id");
+    if (w->comm) return fail(RB_EINVAL, "communicator already initialised");
+    if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
+    HIPCHK(hipSetDevice(w->device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclResult_t r = rccl().CommInitRank(&w->comm, (int)w->P, u, (int)w->rank);
+    if (r != ncclSuccess) { w->comm = nullptr; return fail(RB_ENODEV, "ncclCommInitRank: %s", rccl().GetErrorString(r)); }
+    // first collective outside any graph capture (connection setup); the
+    // snapshot is replicated, so the in-place gather leaves it unchanged
+    char *buf = static_cast<char *>(w->snap[w->sp()]);
+    const size_t n = (size_t)4 * w->S;
+    r = rccl().AllGather(buf + (size_t)w->esz * n * w->rank, buf, n, w->dtype == RB_F64 ? ncclFloat64 : ncclFloat32,
+                         w->comm, w->stream);
+    if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);
+    return RB_OK;
+}
+
+int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    return enqueue_steps(w, nsteps, dt, e, mu, thr, true);
 }
 
 int rb_record_contacts(rb_world *w, int enable) {

@@ -55,6 +55,9 @@ SIGNATURES = {
     "rb_shard_step": (C.c_int, [_P, _D, _D, _D, _D]),
     "rb_shard_exchange_done": (C.c_int, [_P]),
     "rb_gpos_buffer": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(_I64), C.POINTER(_I32)]),
+    "rb_comm_unique_id": (C.c_int, [_P, _I32]),
+    "rb_shard_comm_init": (C.c_int, [_P, _P, _I32]),
+    "rb_shard_run": (C.c_int, [_P, _I64, _D, _D, _D, _D]),
     "rb_record_contacts": (C.c_int, [_P, C.c_int]),
     "rb_get_contacts": (C.c_int, [_P, _P, _P, _P, _P, _I64, C.POINTER(_I64)]),
     "rb_kat_impulse": (C.c_int, [_I32, _I32, _I64, _P, _P]),

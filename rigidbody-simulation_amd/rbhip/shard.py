@@ -8,13 +8,23 @@ body updated from step-start data), and the reference treats a contact
 partner as static (collision.py:27), so a rank needs only the step-start
 POSITIONS of other ranks' bodies.  Per step:
 
-    rb_shard_step           owned bodies: contacts + impulses + integrate;
+    step kernel             owned bodies: contacts + impulses + integrate;
                             new positions land in this rank's slice of the
-                            replicated [P][3][S] position buffer
-    all_gather_into_tensor  RCCL over xGMI (backend "nccl"), in place on the
-                            library's buffer, on the library's stream
-    rb_shard_exchange_done  publish the other ranks' positions to the
+                            replicated [P][S][4] position buffer
+    all-gather              RCCL over xGMI, in place on that buffer
+    remote insert           publish the other ranks' positions to the
                             broadphase of the next step
+
+Transports:
+    "rccl"   (default on an nccl process group) the library owns an RCCL
+             communicator (id broadcast once through torch.distributed) and
+             runs all three per step itself: rb_shard_run replays K steps
+             from one captured HIP graph, no host work per step;
+    "nccl"   rb_shard_step, torch.distributed.all_gather_into_tensor on the
+             library's buffer and stream, rb_shard_exchange_done (three host
+             calls per step);
+    "host"   the same through host memory, for gloo groups (several ranks
+             sharing one GPU in tests).
 
 Contacts are generated from identical global positions with global body
 ids in a canonical order, so fp64 results are bit-identical for any P.
@@ -51,9 +61,10 @@ def wrap_gpos(world: World, torch):
 class ShardedWorld:
     """One rank's shard of a scene; `step` runs the exchange each step.
 
-    transport: "nccl" (RCCL all-gather on device memory; the default when the
-    process group backend is nccl) or "host" (stage through host memory, for
-    gloo process groups, e.g. several ranks sharing one GPU in tests).
+    transport: "rccl" (in-library RCCL exchange, graph-replayed; the default
+    when the process group backend is nccl), "nccl" (torch.distributed
+    all-gather per step) or "host" (stage through host memory, for gloo
+    process groups, e.g. several ranks sharing one GPU in tests).
 
     `world_factory(rank, world_size)` may supply the per-rank stepper (any
     object with the World shard interface and an `exchange_buffer(torch)`
@@ -71,7 +82,8 @@ class ShardedWorld:
             backend = dist.get_backend(group)
         else:
             self.rank, self.P, backend = 0, 1, None
-        self.transport = transport or ("nccl" if backend == "nccl" else "host")
+        self.transport = transport or ("rccl" if backend == "nccl" and world_factory is None else
+                                       "nccl" if backend == "nccl" else "host")
         self._views = {}
         if world_factory is not None:
             self.world = world_factory(self.rank, self.P)
@@ -83,6 +95,12 @@ class ShardedWorld:
                                **world_kw)
             self.stream = torch.cuda.current_stream(device)
             self.world.set_stream(self.stream.cuda_stream)
+        if self.transport == "rccl":
+            # rank 0 of the group makes the communicator id, every rank joins
+            uid = [World.comm_unique_id() if self.rank == 0 else None]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(uid, src=src, group=group)
+            self.world.shard_comm_init(uid[0])
 
     def _buffer(self):
         """(whole buffer, this rank's slice) of the pending exchange; the two
@@ -110,6 +128,9 @@ class ShardedWorld:
             buf.copy_(out.to(buf.device))
 
     def step(self, nsteps: int = 1, **params):
+        if self.transport == "rccl":
+            self.world.shard_run(nsteps, **params)
+            return
         if self.P == 1:
             self.world.step_async(nsteps, **params)
             return
@@ -127,7 +148,7 @@ class ShardedWorld:
         if self.P == 1:
             return q, v
         t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
-        if self.transport == "nccl":
+        if self.transport in ("nccl", "rccl"):
             t = t.to(f"cuda:{self.torch.cuda.current_device()}")
         elif t.dtype != self.torch.float64:
             t = t.double()

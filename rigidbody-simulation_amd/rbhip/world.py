@@ -15,6 +15,8 @@ import numpy as np
 from . import _lib
 from .scenes import Scene
 
+COMM_ID_BYTES = 128      # ncclUniqueId (rccl.h NCCL_UNIQUE_ID_BYTES)
+
 
 class World:
     def __init__(self, scene: Scene, device: int = 0, dtype: str = "f64", rank: int = 0,
@@ -136,10 +138,30 @@ class World:
 
     def gpos_buffer(self):
         """(device pointer, elements per shard, bytes per element) of the
-        replicated [P][3][S] position buffer."""
+        replicated [P][S][4] position buffer."""
         p, n, b = C.c_void_p(), C.c_int64(), C.c_int32()
         _lib.check(self._L.rb_gpos_buffer(self._h, C.byref(p), C.byref(n), C.byref(b)), "rb_gpos_buffer")
         return p.value, n.value, b.value
+
+    # ---- in-library exchange (RCCL communicator owned by the world) ---------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """A new communicator id (rank 0 makes it, every rank joins with it)."""
+        L = _lib.load()
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        _lib.check(L.rb_comm_unique_id(buf, COMM_ID_BYTES), "rb_comm_unique_id")
+        return buf.raw
+
+    def shard_comm_init(self, uid: bytes):
+        """Join the world's ranks in one RCCL communicator (blocks until all have)."""
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"communicator id must be {COMM_ID_BYTES} bytes")
+        _lib.check(self._L.rb_shard_comm_init(self._h, C.c_char_p(uid), COMM_ID_BYTES), "rb_shard_comm_init")
+
+    def shard_run(self, nsteps: int = 1, dt=None, restitution=None, friction=None, threshold=None):
+        """nsteps sharded steps with the in-library exchange (enqueued only)."""
+        p = self._params(dt, restitution, friction, threshold)
+        _lib.check(self._L.rb_shard_run(self._h, int(nsteps), *p), "rb_shard_run")
 
     # ---- parity support -----------------------------------------------------
     def record_contacts(self, enable: bool = True):

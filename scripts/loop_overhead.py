@@ -53,3 +53,10 @@ with rbhip.World(sc) as w:
             w.shard_exchange_done()
     shard_loop_torch()
     print("... + torch op        host %.2f us/step  device %.2f us/step" % timed(shard_loop_torch))
+
+    # the in-library exchange: step kernel + RCCL all-gather (one rank: the
+    # collective's launch and its kernel, no peers) + remote insert, K steps
+    # replayed from one captured graph
+    w.shard_comm_init(rbhip.World.comm_unique_id())
+    w.shard_run(K); torch.cuda.synchronize()
+    print("shard_run (RCCL, 1 rk) host %.2f us/step  device %.2f us/step" % timed(lambda: w.shard_run(K)))

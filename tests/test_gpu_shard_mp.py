@@ -55,3 +55,73 @@ def test_two_process_shards_match_single_world(tmp_path, P):
     mp.start_processes(_worker, args=(P, _free_port(), steps, out), nprocs=P, start_method="spawn")
     got = np.load(out)
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
+
+
+# ---------------------------------------------------------------- in-library RCCL exchange
+# One GPU on the test box: RCCL refuses two ranks on one device, so the
+# in-library exchange is exercised with a one-rank communicator (the
+# all-gather is then a no-op, the graph capture of step + collective +
+# remote insert is real).  The multi-rank data path is the same three
+# operations as the host-staged test above.
+
+def test_inlibrary_exchange_one_rank_matches_world():
+    import rbhip
+    from rbhip import scenes
+    sc = scenes.flat_spheres(24, 24, seed=5)
+    with rbhip.World(sc) as ref:
+        ref.step(613)
+        q1, v1 = ref.get_state()
+    with rbhip.World(sc) as w:
+        w.shard_comm_init(rbhip.World.comm_unique_id())
+        for n in (1, 12, 600):              # eager, one graph, a 512 + 88 chunked replay
+            w.shard_run(n)
+        w.sync()
+        q2, v2 = w.get_state()
+    assert np.array_equal(q1, q2) and np.array_equal(v1, v2)
+
+
+def test_inlibrary_exchange_requires_comm():
+    import rbhip
+    from rbhip import scenes
+    with rbhip.World(scenes.flat_spheres(4, 4)) as w:
+        with pytest.raises(rbhip.RbError):
+            w.shard_run(3)
+
+
+def _rccl_worker(rank, P, port, steps, out):
+    for pth in (ROOT, PKG):
+        sys.path.insert(0, pth)
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=P, device_id=torch.device("cuda:0"))
+    from rbhip import scenes
+    from rbhip.shard import ShardedWorld
+    sc = scenes.tiled(scenes.flat_spheres, P, 16, 16, seed=2)
+    sw = ShardedWorld(sc, device=0)
+    assert sw.transport == "rccl"
+    sw.step(steps)
+    sw.sync()
+    q, v = sw.gather_state()
+    if rank == 0:
+        np.save(out, np.concatenate([q, v], axis=1))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_world_rccl_transport_one_rank(tmp_path):
+    """ShardedWorld on an nccl process group picks the in-library exchange
+    (communicator id broadcast through torch.distributed)."""
+    import torch.multiprocessing as mp
+    import rbhip
+    from rbhip import scenes
+    steps = 80
+    sc = scenes.tiled(scenes.flat_spheres, 1, 16, 16, seed=2)
+    with rbhip.World(sc) as w:
+        w.step(steps)
+        q1, v1 = w.get_state()
+    out = str(tmp_path / "state.npy")
+    mp.start_processes(_rccl_worker, args=(1, _free_port(), steps, out), nprocs=1, start_method="spawn")
+    got = np.load(out)
+    assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
