@@ -31,10 +31,13 @@ ids in a canonical order, so fp64 results are bit-identical for any P.
 """
 from __future__ import annotations
 
+import os
+import warnings
 from typing import Optional
 
 import numpy as np
 
+from ._lib import RbError
 from .scenes import Scene
 from .world import World
 
@@ -82,8 +85,9 @@ class ShardedWorld:
             backend = dist.get_backend(group)
         else:
             self.rank, self.P, backend = 0, 1, None
-        self.transport = transport or ("rccl" if backend == "nccl" and world_factory is None else
-                                       "nccl" if backend == "nccl" else "host")
+        self.transport = (transport or os.environ.get("RBHIP_SHARD_TRANSPORT") or
+                          ("rccl" if backend == "nccl" and world_factory is None else
+                           "nccl" if backend == "nccl" else "host"))
         self._views = {}
         if world_factory is not None:
             self.world = world_factory(self.rank, self.P)
@@ -96,11 +100,21 @@ class ShardedWorld:
             self.stream = torch.cuda.current_stream(device)
             self.world.set_stream(self.stream.cuda_stream)
         if self.transport == "rccl":
-            # rank 0 of the group makes the communicator id, every rank joins
-            uid = [World.comm_unique_id() if self.rank == 0 else None]
-            src = dist.get_global_rank(group, 0) if group is not None else 0
-            dist.broadcast_object_list(uid, src=src, group=group)
-            self.world.shard_comm_init(uid[0])
+            # rank 0 of the group makes the communicator id, every rank joins;
+            # without RCCL in this process every rank takes the torch path
+            uid = [None]
+            if self.rank == 0:
+                try:
+                    uid[0] = World.comm_unique_id()
+                except RbError as e:
+                    warnings.warn(f"in-library RCCL exchange unavailable ({e}); using torch.distributed")
+            if self.P > 1:
+                src = dist.get_global_rank(group, 0) if group is not None else 0
+                dist.broadcast_object_list(uid, src=src, group=group)
+            if uid[0] is None:
+                self.transport = "nccl"
+            else:
+                self.world.shard_comm_init(uid[0])
 
     def _buffer(self):
         """(whole buffer, this rank's slice) of the pending exchange; the two
