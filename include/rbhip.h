@@ -172,6 +172,20 @@ int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes);
 int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double restitution,
                  double friction, double contact_threshold);
 
+/* Peer-to-peer exchange (SURVEY §7 hard part 4), in place of the RCCL
+ * all-gather: after its step kernel each rank flags "step done" into every
+ * peer's flag word, and its exchange kernel reads the other ranks' fresh
+ * slices straight from their buffers over xGMI (IPC mappings) once they
+ * have flagged, then inserts them.  Waits are bounded: a peer missing for
+ * 5 s raises RB_ENODEV at the next rb_sync instead of hanging.
+ *   rb_p2p_handles: this rank's IPC handles (*len bytes; out = NULL to ask
+ *     the size); every rank passes the concatenation of all ranks' handles,
+ *     in rank order, to
+ *   rb_p2p_connect (collective: no rank may step before all have connected).
+ * rb_shard_run then uses this transport; bit-identical to the others. */
+int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len);
+int rb_p2p_connect(rb_world *w, const void *all, int64_t len);
+
 /* ---- the two-ball law -------------------------------------------------- */
 /* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
  * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;

@@ -57,6 +57,7 @@ int64_t next_pow2(int64_t v) {
 }
 
 int err_to_code(int32_t bits) {
+    if (bits & ERR_EXCHANGE) return fail(RB_ENODEV, "device: peer-to-peer exchange timed out (a peer rank did not reach the step)");
     if (bits & ERR_DOMAIN) return fail(RB_EDOM, "device: non-finite or out-of-range body position");
     if (bits & ERR_UNSUPPORTED)
         return fail(RB_EUNSUPPORTED, "device: box-box / box-sphere pair within contact range (not restated)");
@@ -100,6 +101,13 @@ struct rb_world {
     int32_t *err = nullptr;
     int32_t *err_host = nullptr;   // pinned
     ncclComm_t comm = nullptr;     // rb_shard_comm_init: the in-library exchange
+    // peer-to-peer exchange (rb_p2p_connect)
+    bool p2p = false;
+    int64_t *flags = nullptr;      // [P] uncached: peer q writes slot q when its step is done
+    int64_t *epoch = nullptr;      // steps taken since connect (advanced by the step kernel)
+    void **peer_snap_dev = nullptr;       // [2][P] device array: each rank's snapshot buffers
+    int64_t **peer_flags_dev = nullptr;   // [P] device array: each rank's flag array
+    std::vector<void *> ipc_opened;       // peer mappings to close
     // recording
     bool record = false;
     int32_t *rec_count = nullptr, *rec_partner = nullptr, *rec_kind = nullptr;
@@ -165,6 +173,7 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.next = insert_next ? table<T>(w, (ph + 1) % 3, 1 - sp) : Table<T>{nullptr, nullptr, nullptr};
     p.cnt_clear = w->cnt[(ph + 2) % 3];
     p.err = w->err;
+    p.epoch = w->p2p ? w->epoch : nullptr;
     p.plist = w->plist;
     p.plist_cnt = w->plist_cnt;
     if (w->vel[0]) {
@@ -303,12 +312,40 @@ Rccl &rccl() {
     return r;
 }
 
+// the peer-to-peer exchange of the next snapshot (parity nsp, table nph)
+template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp, int nph) {
+    P2PParams<T> pp{};
+    pp.ins = make_insert<T>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local);
+    pp.dst = dp<Snap<T>>(w->snap[nsp], 0);
+    pp.peer_snap = reinterpret_cast<const Snap<T> *const *>(w->peer_snap_dev + (size_t)nsp * w->P);
+    pp.peer_flags = w->peer_flags_dev;
+    pp.flags = w->flags;
+    pp.epoch = w->epoch;
+    pp.rank = (int32_t)w->rank;
+    pp.P = (int32_t)w->P;
+    pp.S = w->S;
+    pp.timeout_ticks = 500000000;      // 5 s at 100 MHz
+    return pp;
+}
+
 // The in-library exchange after the step kernel of step c (which put the own
 // bodies' new positions in this rank's slice of the next snapshot): the
 // in-place all-gather of that snapshot, then the insert of every other
 // rank's bodies into the next table (as rb_shard_exchange_done).
 int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
     const int nsp = 1 - (int)(c % 2), nph = (int)((c + 1) % 3);
+    if (w->p2p) {
+        hipError_t pe;
+        if (w->dtype == RB_F64) {
+            P2PParams<double> pp = make_p2p<double>(w, nsp, nph);
+            pe = launch_p2p_exchange<double>(pp, s);
+        } else {
+            P2PParams<float> pp = make_p2p<float>(w, nsp, nph);
+            pe = launch_p2p_exchange<float>(pp, s);
+        }
+        HIPCHK(pe);
+        return RB_OK;
+    }
     char *buf = static_cast<char *>(w->snap[nsp]);
     const size_t n = (size_t)4 * w->S;
     const ncclResult_t r = rccl().AllGather(buf + (size_t)w->esz * n * w->rank, buf, n,
@@ -336,7 +373,7 @@ void drop_graphs(rb_world *w) {
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
     if (!sharded && w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_run or rb_shard_step + exchange");
-    if (sharded && !w->comm) return fail(RB_EINVAL, "rb_shard_run before rb_shard_comm_init");
+    if (sharded && !w->comm && !w->p2p) return fail(RB_EINVAL, "rb_shard_run before rb_shard_comm_init or rb_p2p_connect");
     if (sharded && w->law != RB_LAW_MUJOCO) return fail(RB_EUNSUPPORTED, "sharded stepping supports the default contact law only");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0))
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
@@ -480,6 +517,10 @@ void free_world(rb_world *w) {
     (void)hipSetDevice(w->device);
     drop_graphs(w);
     if (w->comm) (void)rccl().CommDestroy(w->comm);
+    for (void *q : w->ipc_opened) (void)hipIpcCloseMemHandle(q);
+    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_flags_dev};
+    for (void *b : p2pbufs)
+        if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
                     w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
@@ -729,6 +770,68 @@ int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
                          w->comm, w->stream);
     if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
     HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);
+    return RB_OK;
+}
+
+int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
+    if (!w || !len) return fail(RB_EINVAL, "null argument");
+    const int64_t need = 3 * (int64_t)sizeof(hipIpcMemHandle_t);
+    *len = need;
+    if (!out) return RB_OK;
+    if (cap < need) return fail(RB_EINVAL, "handle buffer needs %lld bytes", (long long)need);
+    HIPCHK(hipSetDevice(w->device));
+    if (!w->flags) {
+        // uncached: peers write it over xGMI while this rank's kernels poll it
+        HIPCHK(hipExtMallocWithFlags((void **)&w->flags, sizeof(int64_t) * w->P, hipDeviceMallocUncached));
+        HIPCHK(hipMemset(w->flags, 0, sizeof(int64_t) * w->P));
+    }
+    hipIpcMemHandle_t h[3];
+    HIPCHK(hipIpcGetMemHandle(&h[0], w->snap[0]));
+    HIPCHK(hipIpcGetMemHandle(&h[1], w->snap[1]));
+    HIPCHK(hipIpcGetMemHandle(&h[2], w->flags));
+    memcpy(out, h, sizeof(h));
+    return RB_OK;
+}
+
+int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
+    if (!w || !all) return fail(RB_EINVAL, "null argument");
+    const int64_t blob = 3 * (int64_t)sizeof(hipIpcMemHandle_t);
+    if (len != blob * w->P) return fail(RB_EINVAL, "expected %lld bytes of handles (P blobs)", (long long)(blob * w->P));
+    if (!w->flags) return fail(RB_EINVAL, "rb_p2p_handles first");
+    if (w->p2p) return fail(RB_EINVAL, "already connected");
+    HIPCHK(hipSetDevice(w->device));
+    std::vector<void *> snaps(2 * (size_t)w->P, nullptr);
+    std::vector<int64_t *> flags((size_t)w->P, nullptr);
+    const char *b = static_cast<const char *>(all);
+    for (int64_t q = 0; q < w->P; ++q) {
+        if (q == w->rank) {
+            snaps[(size_t)q] = w->snap[0];
+            snaps[(size_t)(w->P + q)] = w->snap[1];
+            flags[(size_t)q] = w->flags;
+            continue;
+        }
+        hipIpcMemHandle_t h[3];
+        memcpy(h, b + blob * q, sizeof(h));
+        void *ptr[3] = {};
+        for (int k = 0; k < 3; ++k) {
+            if (hipIpcOpenMemHandle(&ptr[k], h[k], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+                return fail(RB_ENODEV, "hipIpcOpenMemHandle(rank %lld, buffer %d) failed", (long long)q, k);
+            w->ipc_opened.push_back(ptr[k]);
+        }
+        snaps[(size_t)q] = ptr[0];
+        snaps[(size_t)(w->P + q)] = ptr[1];
+        flags[(size_t)q] = static_cast<int64_t *>(ptr[2]);
+    }
+    HIPCHK(hipMalloc((void **)&w->peer_snap_dev, sizeof(void *) * snaps.size()));
+    HIPCHK(hipMalloc((void **)&w->peer_flags_dev, sizeof(int64_t *) * flags.size()));
+    HIPCHK(hipMalloc((void **)&w->epoch, sizeof(int64_t)));
+    HIPCHK(hipMemcpy(w->peer_snap_dev, snaps.data(), sizeof(void *) * snaps.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(w->peer_flags_dev, flags.data(), sizeof(int64_t *) * flags.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(w->epoch, 0, sizeof(int64_t)));
+    HIPCHK(hipMemset(w->flags, 0, sizeof(int64_t) * w->P));
+    HIPCHK(hipDeviceSynchronize());
+    w->p2p = true;
     drop_graphs(w);
     return RB_OK;
 }

@@ -15,6 +15,7 @@ enum : int32_t {
     ERR_PARTNER_OVERFLOW = 2,   // more sphere partners than max_partners
     ERR_UNSUPPORTED = 4,        // box-involved body pair within bounding distance
     ERR_DOMAIN = 8,             // non-finite / out-of-range position
+    ERR_EXCHANGE = 16,          // peer-to-peer exchange: a peer's step did not arrive in time
 };
 
 // Step-start snapshot of one body, indexed by global body id: position and
@@ -112,6 +113,7 @@ template <typename T> struct StepParams {
     Table<T> next;                     // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
     int32_t *cnt_clear;                // counts of the table two steps ahead
     int32_t *err;
+    int64_t *epoch;                    // peer-to-peer exchange: step count, advanced by block 0 (else nullptr)
     // split form only: sorted partner ids [MAXP][S] and counts [S]
     int32_t *plist, *plist_cnt;
     // two-ball law only (rb_balls.hip)
@@ -138,9 +140,26 @@ template <typename T> struct InsertParams {
     int32_t *err;
 };
 
+// Peer-to-peer exchange after a sharded step (rb_p2p.hip): every rank reads
+// the other ranks' fresh snapshot slices straight from their memory (IPC
+// mappings over xGMI), once each peer has flagged its step done, and
+// inserts them into its own next table.
+template <typename T> struct P2PParams {
+    InsertParams<T> ins;               // the local next snapshot's table; skip = own range
+    Snap<T> *dst;                      // the local next snapshot (== ins.snap)
+    const Snap<T> *const *peer_snap;   // [P] each peer's buffer of this parity (own entry unused)
+    int64_t *const *peer_flags;        // [P] each peer's flag array (this rank writes slot rank)
+    const int64_t *flags;              // [P] this rank's flags (uncached; peer q writes slot q)
+    const int64_t *epoch;              // steps taken (written by the preceding step kernel)
+    int32_t rank, P;
+    int64_t S;
+    int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) before ERR_EXCHANGE
+};
+
 // launchers (rb_kernels.hip)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, bool coop, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
+template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s);

@@ -445,6 +445,8 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     asm volatile("" ::"s"(p.snap_cur), "s"(p.st.base), "s"(p.st.S), "s"(p.cs.base), "s"(p.cs.Npad), "s"(p.cs.kind),
                  "s"(p.n_local), "s"(p.lo));
 
+    if (p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;   // peer-to-peer exchange: this step's number
+
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < p.n_local;

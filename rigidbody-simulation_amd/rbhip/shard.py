@@ -16,7 +16,12 @@ POSITIONS of other ranks' bodies.  Per step:
                             broadphase of the next step
 
 Transports:
-    "rccl"   (default on an nccl process group) the library owns an RCCL
+    "p2p"    (default on an nccl process group) every rank reads the other
+             ranks' fresh slices straight from their buffers over xGMI (IPC
+             mappings, handles exchanged once through torch.distributed),
+             signalled by device flags: rb_shard_run replays K steps from
+             one captured HIP graph (SURVEY §7 hard part 4);
+    "rccl"   the library owns an RCCL
              communicator (id broadcast once through torch.distributed) and
              runs all three per step itself: rb_shard_run replays K steps
              from one captured HIP graph, no host work per step;
@@ -64,10 +69,11 @@ def wrap_gpos(world: World, torch):
 class ShardedWorld:
     """One rank's shard of a scene; `step` runs the exchange each step.
 
-    transport: "rccl" (in-library RCCL exchange, graph-replayed; the default
-    when the process group backend is nccl), "nccl" (torch.distributed
-    all-gather per step) or "host" (stage through host memory, for gloo
-    process groups, e.g. several ranks sharing one GPU in tests).
+    transport: "p2p" (peer-to-peer reads over IPC mappings, graph-replayed;
+    the default when the process group backend is nccl), "rccl" (in-library
+    RCCL all-gather, graph-replayed), "nccl" (torch.distributed all-gather
+    per step) or "host" (stage through host memory, for gloo process groups,
+    e.g. several ranks sharing one GPU in tests).
 
     `world_factory(rank, world_size)` may supply the per-rank stepper (any
     object with the World shard interface and an `exchange_buffer(torch)`
@@ -86,7 +92,7 @@ class ShardedWorld:
         else:
             self.rank, self.P, backend = 0, 1, None
         self.transport = (transport or os.environ.get("RBHIP_SHARD_TRANSPORT") or
-                          ("rccl" if backend == "nccl" and world_factory is None else
+                          ("p2p" if backend == "nccl" and world_factory is None else
                            "nccl" if backend == "nccl" else "host"))
         self._views = {}
         if world_factory is not None:
@@ -99,6 +105,8 @@ class ShardedWorld:
                                **world_kw)
             self.stream = torch.cuda.current_stream(device)
             self.world.set_stream(self.stream.cuda_stream)
+        if self.transport == "p2p":
+            self._connect_p2p()
         if self.transport == "rccl":
             # rank 0 of the group makes the communicator id, every rank joins;
             # without RCCL in this process every rank takes the torch path
@@ -115,6 +123,40 @@ class ShardedWorld:
                 self.transport = "nccl"
             else:
                 self.world.shard_comm_init(uid[0])
+
+    def _connect_p2p(self):
+        """Exchange IPC handles once and map every peer's buffers; on any
+        failure (on every rank alike) fall back to the RCCL transport."""
+        dist, torch = self.dist, self.torch
+        try:
+            mine = self.world.p2p_handles()
+        except RbError as e:
+            mine = None
+            warnings.warn(f"peer-to-peer exchange unavailable ({e})")
+        blobs = [mine]
+        if self.P > 1:
+            blobs = [None] * self.P
+            dist.all_gather_object(blobs, mine, group=self.group)
+        ok = all(b is not None for b in blobs)
+        connected = False
+        if ok:
+            try:
+                self.world.p2p_connect(b"".join(blobs))
+                connected = True
+            except RbError as e:
+                ok = False
+                warnings.warn(f"peer-to-peer exchange unavailable ({e})")
+        if self.P > 1:
+            dev = f"cuda:{torch.cuda.current_device()}" if dist.get_backend(self.group) == "nccl" else "cpu"
+            t = torch.tensor([1 if ok else 0], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            ok = bool(t.item())
+        if not ok:
+            if connected:
+                raise RuntimeError("peer-to-peer exchange connected on some ranks only")
+            self.transport = "rccl"
+        if self.P > 1:
+            dist.barrier(group=self.group)   # every rank connected before any steps
 
     def _buffer(self):
         """(whole buffer, this rank's slice) of the pending exchange; the two
@@ -142,7 +184,7 @@ class ShardedWorld:
             buf.copy_(out.to(buf.device))
 
     def step(self, nsteps: int = 1, **params):
-        if self.transport == "rccl":
+        if self.transport in ("p2p", "rccl"):
             self.world.shard_run(nsteps, **params)
             return
         if self.P == 1:
@@ -162,7 +204,7 @@ class ShardedWorld:
         if self.P == 1:
             return q, v
         t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
-        if self.transport in ("nccl", "rccl"):
+        if self.transport in ("nccl", "rccl", "p2p"):
             t = t.to(f"cuda:{self.torch.cuda.current_device()}")
         elif t.dtype != self.torch.float64:
             t = t.double()

@@ -158,6 +158,19 @@ class World:
             raise ValueError(f"communicator id must be {COMM_ID_BYTES} bytes")
         _lib.check(self._L.rb_shard_comm_init(self._h, C.c_char_p(uid), COMM_ID_BYTES), "rb_shard_comm_init")
 
+    def p2p_handles(self) -> bytes:
+        """This rank's IPC handles for the peer-to-peer exchange."""
+        n = C.c_int64()
+        _lib.check(self._L.rb_p2p_handles(self._h, None, 0, C.byref(n)), "rb_p2p_handles")
+        buf = C.create_string_buffer(n.value)
+        _lib.check(self._L.rb_p2p_handles(self._h, buf, n.value, C.byref(n)), "rb_p2p_handles")
+        return buf.raw
+
+    def p2p_connect(self, all_handles: bytes):
+        """Map every peer's buffers (all ranks' handles concatenated in rank
+        order); collective: no rank may step before all have connected."""
+        _lib.check(self._L.rb_p2p_connect(self._h, C.c_char_p(all_handles), len(all_handles)), "rb_p2p_connect")
+
     def shard_run(self, nsteps: int = 1, dt=None, restitution=None, friction=None, threshold=None):
         """nsteps sharded steps with the in-library exchange (enqueued only)."""
         p = self._params(dt, restitution, friction, threshold)

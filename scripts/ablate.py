@@ -14,7 +14,7 @@ paths = {}
 for k, v in enumerate(variants):
     out = f"/tmp/librbhip_ablate{k}.so"
     subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
-                   f"{v} -o {out} rb_kernels.hip rb_balls.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
+                   f"{v} -o {out} rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
     paths[v] = out
 import torch  # noqa: E402  (initialise torch's HIP context before the library's)
 torch.cuda.init()

@@ -60,3 +60,11 @@ with rbhip.World(sc) as w:
     w.shard_comm_init(rbhip.World.comm_unique_id())
     w.shard_run(K); torch.cuda.synchronize()
     print("shard_run (RCCL, 1 rk) host %.2f us/step  device %.2f us/step" % timed(lambda: w.shard_run(K)))
+
+# the peer-to-peer exchange with one rank: the exchange kernel's flag
+# handshake and launch, no peer data
+with rbhip.World(sc) as w:
+    w.set_stream(torch.cuda.current_stream().cuda_stream)
+    w.p2p_connect(w.p2p_handles())
+    w.shard_run(K); torch.cuda.synchronize()
+    print("shard_run (p2p, 1 rk)  host %.2f us/step  device %.2f us/step" % timed(lambda: w.shard_run(K)))

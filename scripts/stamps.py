@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.join(ROOT, "rigidbody-simulation_amd"))
 CSRC = os.path.join(ROOT, "rigidbody-simulation_amd", "csrc")
 extra = os.environ.get("EXTRA_FLAGS", "")
 subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
-               f"-DRB_STAMPS=1 {extra} -o /tmp/libstamp.so rb_kernels.hip rb_balls.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
+               f"-DRB_STAMPS=1 {extra} -o /tmp/libstamp.so rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
 from rbhip import _lib, scenes
 import rbhip.world as W
 L = _lib.load("/tmp/libstamp.so")

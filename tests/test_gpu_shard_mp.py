@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, P, port, steps, out):
+def _worker(rank, P, port, steps, out, transport="host"):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -30,8 +30,8 @@ def _worker(rank, P, port, steps, out):
     from rbhip import scenes
     from rbhip.shard import ShardedWorld
     sc = scenes.tiled(scenes.flat_spheres, P, 16, 16, seed=2)
-    sw = ShardedWorld(sc, device=0)
-    assert sw.transport == "host"
+    sw = ShardedWorld(sc, device=0, transport=transport)
+    assert sw.transport == transport
     sw.step(steps)
     sw.sync()
     q, v = sw.gather_state()
@@ -41,8 +41,10 @@ def _worker(rank, P, port, steps, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P", [2])
-def test_two_process_shards_match_single_world(tmp_path, P):
+@pytest.mark.parametrize("P,transport", [(2, "host"), (2, "p2p"), (3, "p2p")])
+def test_two_process_shards_match_single_world(tmp_path, P, transport):
+    """Several processes on one GPU; "p2p" maps the other processes' buffers
+    through IPC and synchronises on device flags, as across GPUs."""
     import torch.multiprocessing as mp
     import rbhip
     from rbhip import scenes
@@ -52,7 +54,7 @@ def test_two_process_shards_match_single_world(tmp_path, P):
         w.step(steps)
         q1, v1 = w.get_state()
     out = str(tmp_path / "state.npy")
-    mp.start_processes(_worker, args=(P, _free_port(), steps, out), nprocs=P, start_method="spawn")
+    mp.start_processes(_worker, args=(P, _free_port(), steps, out, transport), nprocs=P, start_method="spawn")
     got = np.load(out)
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
 
@@ -88,7 +90,7 @@ def test_inlibrary_exchange_requires_comm():
             w.shard_run(3)
 
 
-def _rccl_worker(rank, P, port, steps, out):
+def _nccl_group_worker(rank, P, port, steps, out, transport, expect):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -99,8 +101,8 @@ def _rccl_worker(rank, P, port, steps, out):
     from rbhip import scenes
     from rbhip.shard import ShardedWorld
     sc = scenes.tiled(scenes.flat_spheres, P, 16, 16, seed=2)
-    sw = ShardedWorld(sc, device=0)
-    assert sw.transport == "rccl"
+    sw = ShardedWorld(sc, device=0, transport=transport)
+    assert sw.transport == expect
     sw.step(steps)
     sw.sync()
     q, v = sw.gather_state()
@@ -110,9 +112,11 @@ def _rccl_worker(rank, P, port, steps, out):
     dist.destroy_process_group()
 
 
-def test_sharded_world_rccl_transport_one_rank(tmp_path):
-    """ShardedWorld on an nccl process group picks the in-library exchange
-    (communicator id broadcast through torch.distributed)."""
+@pytest.mark.parametrize("transport,expect", [(None, "p2p"), ("rccl", "rccl")])
+def test_sharded_world_on_nccl_group_one_rank(tmp_path, transport, expect):
+    """ShardedWorld on an nccl process group: the peer-to-peer exchange by
+    default, or the in-library RCCL exchange (communicator id broadcast
+    through torch.distributed)."""
     import torch.multiprocessing as mp
     import rbhip
     from rbhip import scenes
@@ -122,6 +126,7 @@ def test_sharded_world_rccl_transport_one_rank(tmp_path):
         w.step(steps)
         q1, v1 = w.get_state()
     out = str(tmp_path / "state.npy")
-    mp.start_processes(_rccl_worker, args=(1, _free_port(), steps, out), nprocs=1, start_method="spawn")
+    mp.start_processes(_nccl_group_worker, args=(1, _free_port(), steps, out, transport, expect), nprocs=1,
+                       start_method="spawn")
     got = np.load(out)
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
