@@ -130,3 +130,37 @@ def test_sharded_world_on_nccl_group_one_rank(tmp_path, transport, expect):
                        start_method="spawn")
     got = np.load(out)
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
+
+
+def _timeout_worker(rank, P, port, out):
+    for pth in (ROOT, PKG):
+        sys.path.insert(0, pth)
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    import rbhip
+    from rbhip import scenes
+    from rbhip.shard import ShardedWorld
+    sw = ShardedWorld(scenes.tiled(scenes.flat_spheres, P, 8, 8, seed=1), device=0, transport="p2p")
+    msg = "no error"
+    if rank == 0:                      # rank 1 never steps: rank 0's exchange must give up, not hang
+        sw.step(4)
+        try:
+            sw.sync()
+        except rbhip.RbError as e:
+            msg = str(e)
+        with open(out, "w") as f:
+            f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_p2p_exchange_times_out_instead_of_hanging(tmp_path):
+    import time
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "msg.txt")
+    t0 = time.time()
+    mp.start_processes(_timeout_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    msg = open(out).read()
+    assert "exchange timed out" in msg, msg
+    assert time.time() - t0 < 60
