@@ -168,7 +168,7 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic (seeded rbhip.scenes, SURVEY 8d)",
         "config": {"workload": desc, "bodies_total": scene.n, "bodies_per_gpu": w.n_owned,
-                   "parallelism": f"body-range shards x{P}" + (", in-library RCCL all-gather of positions, graph-replayed" if P > 1 else ""),
+                   "parallelism": f"body-range shards x{P}" + (f", {sw.transport} position exchange, graph-replayed" if P > 1 else ""),
                    "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
