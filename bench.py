@@ -102,13 +102,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     P = max(world_size, 1)
-    torch.cuda.set_device(local_rank)
+    # RBHIP_BENCH_BACKEND=gloo (with RBHIP_SHARD_TRANSPORT=p2p) rehearses the
+    # multi-rank path with several ranks sharing the visible GPUs; its
+    # numbers are not measurements
+    backend = os.environ.get("RBHIP_BENCH_BACKEND", "nccl")
+    device = local_rank if backend == "nccl" else local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(device)
     if P > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group(backend)
     from rbhip.shard import ShardedWorld
 
     scene, desc = make_scene(args.config, P)
-    sw = ShardedWorld(scene, dtype=args.dtype, device=local_rank)
+    sw = ShardedWorld(scene, dtype=args.dtype, device=device)
     w = sw.world
 
     def barrier_sync():
@@ -133,7 +141,7 @@ def main():
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
     if P > 1:
-        t = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=f"cuda:{device}" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
