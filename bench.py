@@ -1,15 +1,25 @@
 """Benchmark: body-steps/s of the rigid-body hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--dtype f64]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--dtype f64]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
-Workload (BASELINE.json configs[1], the metric's single-GPU config): C2 —
-4,096 spheres r 0.1 on flat ground, e 0.8, mu 0.3, dt 0.01, fp64, seeded
-synthetic initial conditions (rbhip.scenes.flat_spheres).  A "step" is one
-reference step of the whole scene (contacts, impulses, integration).  With
-N ranks the scene is N such 64x64 patches side by side on one shared ground
-(weak scaling: 4,096 bodies per GPU); rank r owns patch r and the ranks
-all-gather positions over RCCL every step.
+Workload: C3 (BASELINE.json configs[2]) in fp64 — 65,536 spheres r 0.1 on
+flat ground, e 0.8, mu 0.3, dt 0.01, seeded synthetic initial conditions
+(rbhip.scenes.flat_spheres).  That is the scene the north-star
+target is quoted on ("≥1M body-steps/sec on a 65 536-sphere scene at
+1×MI355X with ≥3.5× at 8 GPUs"); `--config c2` runs configs[1] (4,096
+spheres), c4 / c5 the incline and cube scenes.  A "step" is one reference
+step of the whole scene (contacts, impulses, integration).  With N ranks
+the scene is N such 256x256 patches side by side on one shared ground (weak
+scaling: 65,536 bodies per GPU); rank r owns patch r, and the ranks exchange
+positions inside the library every step (peer-to-peer over xGMI: halo
+pushes for shards this large).
+
+N > 1 is validated: after the warmup and again after the timed region, every
+rank's bodies must be bit-identical to one World of the whole scene stepped
+the same number of steps on rank 0's GPU.  A transport that fails the first
+check (or times out) is replaced by the next (p2p -> rccl); one that fails
+the second makes the run exit non-zero instead of printing a number.
 
 value = total bodies x K / (max over ranks of the timed region), with the
 state resident in HBM.  roofline: algorithmic HBM bytes of the step kernel
@@ -19,8 +29,9 @@ stream (torch's current stream) around the timed region, which is exactly K
 graph-replayed step-kernel launches, / K.  Several ranks: an event pair
 around each step-kernel launch over a second run of K steps.
 cpu_baseline: the oracle (C restatement of the reference arithmetic) on rank 0
-at N=1 over the full C2 scene for 2,000 steps, on the GPU's host-core share
-(OMP_NUM_THREADS, 16 on the GPU box) and on one core.
+at N=1 over the full single-GPU scene for --cpu-steps steps from t = 0, on
+the GPU's host-core share (OMP_NUM_THREADS, 16 on the GPU box) and on one
+core.
 """
 from __future__ import annotations
 
@@ -41,10 +52,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2000)
+    ap.add_argument("--cpu-steps", type=int, default=200)
     return ap.parse_args()
 
 
@@ -82,6 +93,49 @@ def cpu_baseline(cfg: str, steps: int):
                       f"{rates[cores][1]:.1f} s, 1 thread {rates[1][1]:.1f} s"}
 
 
+class SingleWorldCheck:
+    """N > 1: compare every rank's bodies, bit for bit, with one World of the
+    whole scene stepped on rank 0's GPU (collective: every rank calls it
+    with the same step count)."""
+
+    def __init__(self, scene, dtype, device, rank, P):
+        self.scene, self.dtype, self.device, self.rank, self.P = scene, dtype, device, rank, P
+        self.ref, self.done = None, 0
+
+    def __call__(self, sw, steps_total) -> bool:
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        ok = 1
+        try:
+            sw.sync()
+        except Exception as e:          # an exchange timeout or a device error
+            print(f"bench: rank {self.rank}: {e}", file=sys.stderr, flush=True)
+            ok = 0
+        dev = f"cuda:{self.device}" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([ok], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if not int(t.item()):
+            return False
+        q, v = sw.gather_state()
+        same = 1
+        if self.rank == 0:
+            import rbhip
+            if self.ref is None:
+                self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype)
+            self.ref.step(steps_total - self.done)
+            self.done = steps_total
+            q1, v1 = self.ref.get_state()
+            same = int(np.array_equal(q, q1) and np.array_equal(v, v1))
+            if not same:
+                bad = np.flatnonzero(~(np.all(q == q1, axis=1) & np.all(v == v1, axis=1)))
+                print(f"bench: {bad.size} bodies differ from the single World after {steps_total} steps "
+                      f"(first ids {bad[:8].tolist()})", file=sys.stderr, flush=True)
+        t = torch.tensor([same], device=dev)
+        dist.broadcast(t, src=0)
+        return bool(int(t.item()))
+
+
 def traffic_from_profiles(cfg: str, dtype: str):
     """HBM bytes per step-kernel launch from the committed PMC summary
     (profiles/pmc_traffic.json, written by profiles/collect_pmc.py)."""
@@ -116,8 +170,23 @@ def main():
     from rbhip.shard import ShardedWorld
 
     scene, desc = make_scene(args.config, P)
-    sw = ShardedWorld(scene, dtype=args.dtype, device=device)
+    check = SingleWorldCheck(scene, args.dtype, device, rank, P) if P > 1 else None
+    transports = [None, "rccl"] if P > 1 else [None]
+    for k, tr in enumerate(transports):
+        sw = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr)
+        # warmup (also builds and caches the K-step graphs)
+        sw.step(args.warmup)
+        if check is None or check(sw, args.warmup):
+            break
+        name = sw.transport + (" (halo)" if sw.halo else "")
+        sw.world.close()
+        if k + 1 == len(transports):
+            raise SystemExit(f"bench: every transport failed validation (last: {name})")
+        if rank == 0:
+            print(f"bench: {name} exchange failed validation; falling back to {transports[k + 1]}",
+                  file=sys.stderr, flush=True)
     w = sw.world
+    sw.sync()
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -125,9 +194,6 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # warmup (also builds and caches the K-step graphs)
-    sw.step(args.warmup)
-    sw.sync()
     sw.step(args.steps)              # capture the K-step graph outside the timed region
     sw.sync()
     barrier_sync()
@@ -144,6 +210,8 @@ def main():
         t = torch.tensor([elapsed], device=f"cuda:{device}" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        if not check(sw, args.warmup + 2 * args.steps):
+            raise SystemExit("bench: the sharded run diverged from the single-World run during the timed steps")
 
     # roofline: average step-kernel launch duration.  One rank: the timed
     # region is exactly K back-to-back step-kernel launches (graph replay),
@@ -176,8 +244,11 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic (seeded rbhip.scenes, SURVEY 8d)",
         "config": {"workload": desc, "bodies_total": scene.n, "bodies_per_gpu": w.n_owned,
-                   "parallelism": f"body-range shards x{P}" + (f", {sw.transport} position exchange, graph-replayed" if P > 1 else ""),
-                   "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction},
+                   "parallelism": f"body-range shards x{P}" + (
+                       f", {sw.transport}{' halo' if sw.halo else ''} position exchange, graph-replayed" if P > 1 else ""),
+                   "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction,
+                   **({"validated": f"bit-identical to one World of the whole scene after {args.warmup} and "
+                                    f"{args.warmup + 2 * args.steps} steps"} if P > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("rb::step_kernel_coop" if w.n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "32768"))

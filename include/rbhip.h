@@ -186,6 +186,17 @@ int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double restitution,
 int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len);
 int rb_p2p_connect(rb_world *w, const void *all, int64_t len);
 
+/* Halo mode of the peer-to-peer exchange, for large shards (no reference
+ * counterpart: the reference is single-process).  Instead of reading every
+ * peer's whole slice, each rank pushes to each peer only its bodies whose
+ * cell lies within one cell of the cell bounds of that peer's own bodies
+ * (a superset of everything the peer's contact searches can reach), into
+ * the peer's inbox, after the ranks have exchanged those bounds.  Two
+ * kernels per step, no host work; still bit-identical to every other
+ * transport.  Collective: every rank must make the same call, after
+ * rb_p2p_connect and before stepping.  enable = 0 returns to full reads. */
+int rb_p2p_halo(rb_world *w, int32_t enable);
+
 /* ---- the two-ball law -------------------------------------------------- */
 /* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
  * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;

@@ -103,7 +103,11 @@ struct rb_world {
     ncclComm_t comm = nullptr;     // rb_shard_comm_init: the in-library exchange
     // peer-to-peer exchange (rb_p2p_connect)
     bool p2p = false;
-    int64_t *flags = nullptr;      // [P] uncached: peer q writes slot q when its step is done
+    int64_t *flags = nullptr;      // the mailbox (MailLayout, uncached); starts with flags[P]: peer q
+                                   // writes slot q when its step is done
+    bool halo = false;             // rb_p2p_halo: push only the bodies a peer can reach
+    int32_t *bounds = nullptr;     // halo: [2][BOUND_COPIES][BOUND_STRIDE] own cell bounds (step parity)
+    int32_t *push_cnt = nullptr;   // halo: [P] bodies pushed to each peer this step
     int64_t *epoch = nullptr;      // steps taken since connect (advanced by the step kernel)
     void **peer_snap_dev = nullptr;       // [2][P] device array: each rank's snapshot buffers
     int64_t **peer_flags_dev = nullptr;   // [P] device array: each rank's flag array
@@ -174,6 +178,7 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.cnt_clear = w->cnt[(ph + 2) % 3];
     p.err = w->err;
     p.epoch = w->p2p ? w->epoch : nullptr;
+    p.bounds = w->halo ? w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE : nullptr;
     p.plist = w->plist;
     p.plist_cnt = w->plist_cnt;
     if (w->vel[0]) {
@@ -328,12 +333,39 @@ template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp, int nph) {
     return pp;
 }
 
+// the halo exchange after the step kernel of step c (next snapshot nsp, table nph)
+template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp, int nph) {
+    HaloParams<T> hp{};
+    hp.ins = make_insert<T>(w, nsp, nph, 0, 0, 0, 0);
+    hp.dst = dp<Snap<T>>(w->snap[nsp], 0);
+    hp.bounds = w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE;
+    hp.bounds_reset = w->bounds + ((c + 1) % 2) * BOUND_COPIES * BOUND_STRIDE;
+    hp.push_cnt = w->push_cnt;
+    hp.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
+    hp.mail = reinterpret_cast<const char *>(w->flags);
+    hp.lay = MailLayout::make(w->P, w->S, w->esz);
+    hp.epoch = w->epoch;
+    hp.rank = (int32_t)w->rank;
+    hp.P = (int32_t)w->P;
+    hp.n_local = w->n_local;
+    hp.lo = w->lo;
+    hp.S = w->S;
+    hp.timeout_ticks = 500000000;      // 5 s at 100 MHz
+    return hp;
+}
+
 // The in-library exchange after the step kernel of step c (which put the own
 // bodies' new positions in this rank's slice of the next snapshot): the
 // in-place all-gather of that snapshot, then the insert of every other
 // rank's bodies into the next table (as rb_shard_exchange_done).
 int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
     const int nsp = 1 - (int)(c % 2), nph = (int)((c + 1) % 3);
+    if (w->p2p && w->halo) {
+        const hipError_t he = w->dtype == RB_F64 ? launch_halo_exchange<double>(make_halo<double>(w, c, nsp, nph), s)
+                                                 : launch_halo_exchange<float>(make_halo<float>(w, c, nsp, nph), s);
+        HIPCHK(he);
+        return RB_OK;
+    }
     if (w->p2p) {
         hipError_t pe;
         if (w->dtype == RB_F64) {
@@ -518,7 +550,7 @@ void free_world(rb_world *w) {
     drop_graphs(w);
     if (w->comm) (void)rccl().CommDestroy(w->comm);
     for (void *q : w->ipc_opened) (void)hipIpcCloseMemHandle(q);
-    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_flags_dev};
+    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_flags_dev, w->bounds, w->push_cnt};
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -782,9 +814,11 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
     if (cap < need) return fail(RB_EINVAL, "handle buffer needs %lld bytes", (long long)need);
     HIPCHK(hipSetDevice(w->device));
     if (!w->flags) {
-        // uncached: peers write it over xGMI while this rank's kernels poll it
-        HIPCHK(hipExtMallocWithFlags((void **)&w->flags, sizeof(int64_t) * w->P, hipDeviceMallocUncached));
-        HIPCHK(hipMemset(w->flags, 0, sizeof(int64_t) * w->P));
+        // the mailbox, uncached: peers write it over xGMI while this rank's
+        // kernels poll and read it
+        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz);
+        HIPCHK(hipExtMallocWithFlags((void **)&w->flags, (size_t)lay.bytes, hipDeviceMallocUncached));
+        HIPCHK(hipMemset(w->flags, 0, (size_t)lay.bytes));
     }
     hipIpcMemHandle_t h[3];
     HIPCHK(hipIpcGetMemHandle(&h[0], w->snap[0]));
@@ -833,6 +867,29 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     HIPCHK(hipDeviceSynchronize());
     w->p2p = true;
     drop_graphs(w);
+    return RB_OK;
+}
+
+int rb_p2p_halo(rb_world *w, int32_t enable) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (!w->p2p) return fail(RB_EINVAL, "rb_p2p_halo before rb_p2p_connect");
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (enable) {
+        if (!w->bounds) {
+            HIPCHK(hipMalloc((void **)&w->bounds, sizeof(int32_t) * 2 * BOUND_COPIES * BOUND_STRIDE));
+            HIPCHK(hipMalloc((void **)&w->push_cnt, sizeof(int32_t) * w->P));
+        }
+        // both parities empty: the next step kernel accumulates into one, its
+        // push kernel resets the other
+        std::vector<int32_t> b((size_t)2 * BOUND_COPIES * BOUND_STRIDE, 0);
+        for (int k = 0; k < 2 * BOUND_COPIES; ++k)
+            for (int d = 0; d < 3; ++d) { b[(size_t)k * BOUND_STRIDE + d] = INT32_MAX; b[(size_t)k * BOUND_STRIDE + 3 + d] = INT32_MIN; }
+        HIPCHK(hipMemcpy(w->bounds, b.data(), sizeof(int32_t) * b.size(), hipMemcpyHostToDevice));
+        HIPCHK(hipMemset(w->push_cnt, 0, sizeof(int32_t) * w->P));
+    }
+    if (w->halo != (enable != 0)) drop_graphs(w);
+    w->halo = enable != 0;
     return RB_OK;
 }
 

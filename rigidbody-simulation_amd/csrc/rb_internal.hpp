@@ -114,6 +114,8 @@ template <typename T> struct StepParams {
     int32_t *cnt_clear;                // counts of the table two steps ahead
     int32_t *err;
     int64_t *epoch;                    // peer-to-peer exchange: step count, advanced by block 0 (else nullptr)
+    int32_t *bounds;                   // halo exchange: [BOUND_COPIES][BOUND_STRIDE] cell bounds of the
+                                       // own bodies' new positions (atomic min/max; else nullptr)
     // split form only: sorted partner ids [MAXP][S] and counts [S]
     int32_t *plist, *plist_cnt;
     // two-ball law only (rb_balls.hip)
@@ -156,10 +158,60 @@ template <typename T> struct P2PParams {
     int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) before ERR_EXCHANGE
 };
 
+// Halo exchange (rb_p2p.hip), for large shards: instead of reading every
+// peer's whole slice, each rank PUSHES to each peer only its bodies whose
+// cell lies within one cell of that peer's own bodies' cell bounds — a
+// superset of every body the peer's 2x2x2 searches can reach.
+//
+// The own bounds are accumulated by the step kernel with atomic min/max into
+// BOUND_COPIES spread copies (block b uses copy b % BOUND_COPIES, so the
+// atomics do not contend on one line), reduced by the push kernel.
+constexpr int BOUND_COPIES = 64;
+constexpr int BOUND_STRIDE = 32;       // int32 per copy (128 B): min x y z, max x y z, unused
+//
+// Each rank's mailbox is one uncached allocation, written by the peers over
+// xGMI (IPC mappings) and polled / read by this rank:
+//   int64  flags[P]          full-read exchange: "step e done" from peer q
+//   int64  box[P][6]         halo: peer q's cell bounds, (e << 32) | uint32(v)
+//   int64  cnt[P]            halo: bodies peer q pushed, (e << 32) | count
+//   uint32 in_ids[P][S]      halo: pushed ids, region q written by peer q
+//   Snap   in_snap[P][S]     halo: their snapshots
+// Packing the epoch into every word lets a reader tell a fresh word from a
+// stale one without a separate flag (and a release fence before it).
+struct MailLayout {
+    int64_t o_flags, o_box, o_cnt, o_ids, o_snap, bytes;
+    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz) {
+        MailLayout m;
+        m.o_flags = 0;
+        m.o_box = 8 * P;
+        m.o_cnt = m.o_box + 48 * P;
+        m.o_ids = m.o_cnt + 8 * P;
+        m.o_snap = (m.o_ids + 4 * P * S + 255) / 256 * 256;
+        m.bytes = m.o_snap + 4 * esz * P * S;
+        return m;
+    }
+};
+
+template <typename T> struct HaloParams {
+    InsertParams<T> ins;               // the local next snapshot's table (count, skip unused)
+    Snap<T> *dst;                      // the local next snapshot (own rows fresh; pushed rows land here)
+    int32_t *bounds;                   // this step's own-bound copies (from the step kernel)
+    int32_t *bounds_reset;             // the other parity's copies: reset for the next step kernel
+    int32_t *push_cnt;                 // [P] bodies pushed to each peer this step
+    char *const *peer_mail;            // [P] each peer's mailbox (own entry unused)
+    const char *mail;                  // this rank's mailbox
+    MailLayout lay;
+    const int64_t *epoch;
+    int32_t rank, P, n_local;
+    int64_t lo, S;
+    int64_t timeout_ticks;
+};
+
 // launchers (rb_kernels.hip)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, bool coop, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
+template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s);

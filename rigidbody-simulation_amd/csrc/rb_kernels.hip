@@ -280,7 +280,7 @@ template <typename T, bool POS>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, bool forced, LazyInvI<T> &invI,
                                             int32_t np_, const int32_t *pid, int64_t stride, const Snap<T> *ppos,
-                                            int tid) {
+                                            int tid, int32_t *cell) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -365,6 +365,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     Claim cl{0u, -1};
     if (p.next.cnt) cl = claim_slot(p.grid, p.next, p.err, sn);
     wt_store(p.snap_next + i, sn);
+    if (p.bounds) {                              // halo exchange: this body's new cell
+        int32_t cx, cy, cz;
+        if (cell_of(sn.x, sn.y, sn.z, p.grid.inv_cs, cx, cy, cz)) { cell[0] = cx; cell[1] = cy; cell[2] = cz; }
+    }
     STAMP(5);
     const Q4<T> res = mj_mulquat(Q4<T>{T(0), w.x, w.y, w.z}, q);
     Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
@@ -382,7 +386,8 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 // One body (G lanes): contact search, then (lane 0) the update.
 template <typename T, int MAXP, int G>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
-                                          int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos) {
+                                          int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
+                                          int32_t *cell) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = p.lo + l;
@@ -426,7 +431,33 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
         invI.I = in.I;
         invI.q = in.q;
     }
-    body_update<T, (G > 1)>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB, s_pos + slot, tid);
+    body_update<T, (G > 1)>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB, s_pos + slot, tid,
+                            cell);
+}
+
+// Halo exchange: fold the wave's new cells (cell[0] == INT32_MAX: none) into
+// the step's bound copies — one atomic min/max per axis per wave, on copy
+// (block % BOUND_COPIES).  Every lane of the wave must call it.
+__device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell) {
+    int32_t lo[3], hi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const bool have = cell[0] != INT32_MAX;
+        lo[d] = have ? cell[d] : INT32_MAX;
+        hi[d] = have ? cell[d] : INT32_MIN;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = min(lo[d], __shfl_xor(lo[d], off));
+            hi[d] = max(hi[d], __shfl_xor(hi[d], off));
+        }
+    if ((threadIdx.x & 63) == 0 && lo[0] != INT32_MAX) {
+        int32_t *c = bounds + (int64_t)(blockIdx.x % BOUND_COPIES) * BOUND_STRIDE;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { atomicMin(c + d, lo[d]); atomicMax(c + 3 + d, hi[d]); }
+    }
 }
 
 template <typename T, int MAXP, int G>
@@ -450,7 +481,9 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < p.n_local;
-    if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos);
+    int32_t cell[3] = {INT32_MAX, 0, 0};
+    if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, cell);
+    if (p.bounds) fold_bounds(p.bounds, cell);
     // The counts of step t+2's table were last read by step t-1: clear them
     // for step t+1's inserts.  Last, since every load or atomic issued after
     // a store waits for it (vmcnt counts in issue order).
@@ -517,6 +550,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
     const int tid = threadIdx.x;
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
     const int64_t lb = gt;
+    int32_t cell[3] = {INT32_MAX, 0, 0};
     if (lb < p.n_local) {
         const int32_t l = (int32_t)lb, i = p.lo + l;
         const Snap<T> self = p.snap_cur[CHK(i, p.n_global)];
@@ -529,8 +563,10 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
         invI.q = in.q;
         const int32_t np_ = p.plist_cnt[CHK(l, p.S)];
         if (RB_BOUNDS && np_ > 16) printf("RB_BOUNDS np_ %d at l %d\n", np_, l);
-        body_update<T, false>(p, l, i, x, kind, sz, self.r, in, false, invI, np_, p.plist + l, p.S, nullptr, tid);
+        body_update<T, false>(p, l, i, x, kind, sz, self.r, in, false, invI, np_, p.plist + l, p.S, nullptr, tid,
+                              cell);
     }
+    if (p.bounds) fold_bounds(p.bounds, cell);
     for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
 }
 

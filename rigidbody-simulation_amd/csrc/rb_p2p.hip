@@ -53,6 +53,201 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
     insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, (uint32_t)id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u));
 }
 
+// ---- halo exchange (large shards) -----------------------------------------
+// Two kernels after the step kernel of step e (HaloParams, rb_internal.hpp):
+//   push:   block 0 reduces the own cell bounds and stores them, epoch-tagged,
+//           into every peer's mailbox (and resets the other parity's copies);
+//           every block waits for all peers' bounds of step e, then each
+//           thread tests one own body's new cell against each peer's bounds
+//           +-1 cell and, if inside, appends (id, snapshot) to that peer's
+//           inbox (slot from a wave-aggregated atomic on push_cnt[peer]);
+//           each wave ends with a system-scope release (its remote stores
+//           complete before the kernel does);
+//   insert: block 0 stores push_cnt[q], epoch-tagged, into peer q's mailbox
+//           and resets it; every block waits for all peers' counts of step
+//           e, then the grid copies the received snapshots into the next
+//           snapshot buffer and inserts them into the next table.
+// A peer pushes into this rank's inbox for step e+1 only after this rank's
+// bounds of step e+1 reached it, i.e. after this rank's insert of step e
+// finished reading: one inbox per peer suffices.
+// Why exact: a partner j of an own body i lies within reach of i, and the
+// cell size is >= 2 x the reach, so cell(j) is within one cell of cell(i)
+// on every axis — inside the bounds +-1 of i's rank.  Bodies not pushed are
+// never within reach of any body of the receiving rank, and every contact
+// test and its order depend only on the bodies within reach.
+
+__device__ __forceinline__ uint64_t pack_epoch(int64_t e, int32_t v) {
+    return ((uint64_t)e << 32) | (uint32_t)v;
+}
+
+// One lane per peer (lanes 0..63 of the block) waits until word(q) of every
+// peer q != rank carries epoch >= e.  Bounded: after timeout_ticks (or once
+// any exchange timed out) ERR_EXCHANGE is raised and the wait ends.
+template <typename Word>
+__device__ __forceinline__ void wait_peers(int32_t P, int32_t rank, int64_t e, int64_t timeout_ticks, int32_t *err,
+                                           Word word) {
+    const int tid = threadIdx.x;
+    if (tid >= 64) return;
+    const bool need = tid < P && tid != rank;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const bool ok = !need || word(tid) >= e;
+        if (__all(ok)) break;
+        if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > timeout_ticks ||
+            (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_EXCHANGE)) {
+            if (tid == 0) atomicOr(err, ERR_EXCHANGE);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+__device__ __forceinline__ int64_t load_sys(const int64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void store_sys(int64_t *p, int64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void halo_push_kernel(HaloParams<T> p) {
+    const int64_t e = *p.epoch;
+    const int tid = threadIdx.x;
+    const MailLayout &L = p.lay;
+    __shared__ int32_t s_box[64][6];
+    if (blockIdx.x == 0 && tid < 64) {
+        // own bounds: lane k folds copy k; the butterfly leaves the result in every lane
+        const int32_t *c = p.bounds + (int64_t)tid * BOUND_STRIDE;
+        int32_t b[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) b[d] = c[d];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                b[d] = min(b[d], __shfl_xor(b[d], off));
+                b[3 + d] = max(b[3 + d], __shfl_xor(b[3 + d], off));
+            }
+        int32_t *r = p.bounds_reset + (int64_t)tid * BOUND_STRIDE;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { r[d] = INT32_MAX; r[3 + d] = INT32_MIN; }
+        if (tid < p.P && tid != p.rank) {
+            int64_t *box = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_box) + 6 * p.rank;
+#pragma unroll
+            for (int d = 0; d < 6; ++d) store_sys(box + d, (int64_t)pack_epoch(e, b[d]));
+        }
+    }
+    const int64_t *box_in = reinterpret_cast<const int64_t *>(p.mail + L.o_box);
+    wait_peers(p.P, p.rank, e, p.timeout_ticks, p.ins.err, [&](int q) {
+        int64_t lo = INT64_MAX;
+#pragma unroll
+        for (int d = 0; d < 6; ++d) {
+            const int64_t w = (int64_t)((uint64_t)load_sys(box_in + 6 * q + d) >> 32);
+            lo = w < lo ? w : lo;
+        }
+        return lo;
+    });
+    if (tid < 64 && tid < p.P && tid != p.rank)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) s_box[tid][d] = (int32_t)(uint32_t)load_sys(box_in + 6 * tid + d);
+    __syncthreads();
+
+    const int64_t l = (int64_t)blockIdx.x * 256 + tid;
+    const bool active = l < p.n_local;
+    int32_t cx = 0, cy = 0, cz = 0;
+    Snap<T> s{};
+    bool ok = false;
+    if (active) {
+        s = p.dst[p.lo + l];
+        ok = cell_of(s.x, s.y, s.z, p.ins.grid.inv_cs, cx, cy, cz);   // else: ERR_DOMAIN raised by the step
+    }
+    const uint64_t lt = (1ull << (tid & 63)) - 1ull;
+    for (int q = 0; q < p.P; ++q) {
+        if (q == p.rank) continue;
+        const int32_t *b = s_box[q];
+        // empty bounds (min > max): the peer owns no body, needs none.
+        // Compared in int64: min - 1 / max + 1 cannot overflow.
+        const bool in = ok && b[0] <= b[3] && (int64_t)cx >= (int64_t)b[0] - 1 && (int64_t)cx <= (int64_t)b[3] + 1 &&
+                        (int64_t)cy >= (int64_t)b[1] - 1 && (int64_t)cy <= (int64_t)b[4] + 1 &&
+                        (int64_t)cz >= (int64_t)b[2] - 1 && (int64_t)cz <= (int64_t)b[5] + 1;
+        const uint64_t m = __ballot(in);
+        if (m == 0) continue;
+        const int leader = __builtin_ctzll(m);
+        int32_t base = 0;
+        if ((tid & 63) == leader) base = atomicAdd(p.push_cnt + q, __popcll(m));
+        base = __shfl(base, leader);
+        if (in) {
+            const int64_t slot = base + __popcll(m & lt);
+            if (slot < p.S) {       // a peer holds at most S of this rank's bodies
+                char *mail = p.peer_mail[q];
+                uint32_t *ids = reinterpret_cast<uint32_t *>(mail + L.o_ids) + (int64_t)p.rank * p.S;
+                Snap<T> *sn = reinterpret_cast<Snap<T> *>(mail + L.o_snap) + (int64_t)p.rank * p.S;
+                ids[slot] = (uint32_t)(p.lo + l);
+                sn[slot] = s;
+            }
+        }
+    }
+    // the remote stores reach the peer's memory before this kernel completes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
+    const int64_t e = *p.epoch;
+    const int tid = threadIdx.x;
+    const MailLayout &L = p.lay;
+    __shared__ int64_t s_off[65];
+    if (blockIdx.x == 0 && tid < p.P && tid != p.rank) {
+        const int32_t n = p.push_cnt[tid];
+        int64_t *cnt = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_cnt) + p.rank;
+        store_sys(cnt, (int64_t)pack_epoch(e, n < p.S ? n : (int32_t)p.S));
+        p.push_cnt[tid] = 0;
+    }
+    const int64_t *cnt_in = reinterpret_cast<const int64_t *>(p.mail + L.o_cnt);
+    wait_peers(p.P, p.rank, e, p.timeout_ticks, p.ins.err,
+               [&](int q) { return (int64_t)((uint64_t)load_sys(cnt_in + q) >> 32); });
+    if (tid == 0) {
+        int64_t o = 0;
+        for (int q = 0; q < p.P; ++q) {
+            s_off[q] = o;
+            if (q != p.rank) {
+                const int64_t w = load_sys(cnt_in + q);
+                // only a current word counts (a timed-out wait leaves stale ones)
+                if ((int64_t)((uint64_t)w >> 32) == e) o += (int64_t)(uint32_t)w;
+            }
+        }
+        s_off[p.P] = o;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const int64_t total = s_off[p.P];
+    const uint32_t *ids = reinterpret_cast<const uint32_t *>(p.mail + L.o_ids);
+    const Snap<T> *sn = reinterpret_cast<const Snap<T> *>(p.mail + L.o_snap);
+    for (int64_t k = (int64_t)blockIdx.x * 256 + tid; k < total; k += (int64_t)gridDim.x * 256) {
+        int q = 0;
+        while (k >= s_off[q + 1]) ++q;
+        const int64_t o = (int64_t)q * p.S + (k - s_off[q]);
+        const uint32_t id = ids[o];
+        const Snap<T> s = sn[o];
+        if ((int64_t)id < (int64_t)q * p.S || (int64_t)id >= (int64_t)(q + 1) * p.S) {   // not peer q's body
+            atomicOr(p.ins.err, ERR_EXCHANGE);
+            continue;
+        }
+        p.dst[id] = s;
+        insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u));
+    }
+}
+
+template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s) {
+    if (p.P < 1 || p.P > 64 || p.S <= 0) return hipErrorInvalidValue;
+    const int64_t pb = (p.n_local + 255) / 256;
+    hipLaunchKernelGGL((halo_push_kernel<T>), dim3((unsigned)(pb > 0 ? pb : 1)), dim3(256), 0, s, p);
+    int64_t ib = ((int64_t)(p.P - 1) * p.S + 255) / 256;
+    ib = ib < 1 ? 1 : ib > 256 ? 256 : ib;
+    hipLaunchKernelGGL((halo_insert_kernel<T>), dim3((unsigned)ib), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s) {
     if (p.ins.count <= 0 || p.P < 1 || p.P > 64) return hipErrorInvalidValue;
     const int64_t blocks = (p.ins.count + 255) / 256;
@@ -62,5 +257,7 @@ template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipS
 
 template hipError_t launch_p2p_exchange<double>(const P2PParams<double> &, hipStream_t);
 template hipError_t launch_p2p_exchange<float>(const P2PParams<float> &, hipStream_t);
+template hipError_t launch_halo_exchange<double>(const HaloParams<double> &, hipStream_t);
+template hipError_t launch_halo_exchange<float>(const HaloParams<float> &, hipStream_t);
 
 }  // namespace rb

@@ -20,7 +20,10 @@ Transports:
              ranks' fresh slices straight from their buffers over xGMI (IPC
              mappings, handles exchanged once through torch.distributed),
              signalled by device flags: rb_shard_run replays K steps from
-             one captured HIP graph (SURVEY §7 hard part 4);
+             one captured HIP graph (SURVEY §7 hard part 4).  For large
+             shards (halo="auto": >= HALO_MIN_SHARD bodies per rank) the
+             halo mode instead pushes to each peer only the bodies within
+             one cell of the peer's own bodies' cell bounds;
     "rccl"   the library owns an RCCL
              communicator (id broadcast once through torch.distributed) and
              runs all three per step itself: rb_shard_run replays K steps
@@ -45,6 +48,12 @@ import numpy as np
 from ._lib import RbError
 from .scenes import Scene
 from .world import World
+
+# shard size from which the peer-to-peer exchange pushes halos instead of
+# reading whole slices: a halo step costs two kernels and two one-way flag
+# latencies, a full read (P-1) x S x 32 B over xGMI (~28 us for 65,536 fp64
+# bodies from 7 peers at ~75 GB/s per link)
+HALO_MIN_SHARD = 16384
 
 
 class _DeviceBuffer:
@@ -81,7 +90,7 @@ class ShardedWorld:
     `device`."""
 
     def __init__(self, scene: Scene, dtype: str = "f64", device: Optional[int] = None,
-                 group=None, transport: Optional[str] = None, world_factory=None, **world_kw):
+                 group=None, transport: Optional[str] = None, world_factory=None, halo="auto", **world_kw):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -105,8 +114,17 @@ class ShardedWorld:
                                **world_kw)
             self.stream = torch.cuda.current_stream(device)
             self.world.set_stream(self.stream.cuda_stream)
+        self.halo = False
         if self.transport == "p2p":
             self._connect_p2p()
+        if self.transport == "p2p":
+            env = os.environ.get("RBHIP_P2P_HALO")
+            h = {"1": True, "0": False}.get(env, halo) if env else halo
+            if h == "auto":
+                h = -(-scene.n // self.P) >= HALO_MIN_SHARD
+            if h:
+                self.world.p2p_halo(True)
+                self.halo = True
         if self.transport == "rccl":
             # rank 0 of the group makes the communicator id, every rank joins;
             # without RCCL in this process every rank takes the torch path
@@ -204,7 +222,7 @@ class ShardedWorld:
         if self.P == 1:
             return q, v
         t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
-        if self.transport in ("nccl", "rccl", "p2p"):
+        if self.dist.get_backend(self.group) == "nccl":
             t = t.to(f"cuda:{self.torch.cuda.current_device()}")
         elif t.dtype != self.torch.float64:
             t = t.double()

@@ -171,6 +171,11 @@ class World:
         order); collective: no rank may step before all have connected."""
         _lib.check(self._L.rb_p2p_connect(self._h, C.c_char_p(all_handles), len(all_handles)), "rb_p2p_connect")
 
+    def p2p_halo(self, enable: bool = True):
+        """Halo mode of the peer-to-peer exchange (push only the bodies a peer
+        can reach); collective, after p2p_connect."""
+        _lib.check(self._L.rb_p2p_halo(self._h, 1 if enable else 0), "rb_p2p_halo")
+
     def shard_run(self, nsteps: int = 1, dt=None, restitution=None, friction=None, threshold=None):
         """nsteps sharded steps with the in-library exchange (enqueued only)."""
         p = self._params(dt, restitution, friction, threshold)

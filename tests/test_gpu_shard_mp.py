@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, P, port, steps, out, transport="host"):
+def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -29,9 +29,9 @@ def _worker(rank, P, port, steps, out, transport="host"):
     dist.init_process_group("gloo", rank=rank, world_size=P)
     from rbhip import scenes
     from rbhip.shard import ShardedWorld
-    sc = scenes.tiled(scenes.flat_spheres, P, 16, 16, seed=2)
-    sw = ShardedWorld(sc, device=0, transport=transport)
-    assert sw.transport == transport
+    sc = scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2)
+    sw = ShardedWorld(sc, device=0, transport=transport, halo=halo)
+    assert sw.transport == transport and sw.halo == halo
     sw.step(steps)
     sw.sync()
     q, v = sw.gather_state()
@@ -41,20 +41,25 @@ def _worker(rank, P, port, steps, out, transport="host"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P,transport", [(2, "host"), (2, "p2p"), (3, "p2p")])
-def test_two_process_shards_match_single_world(tmp_path, P, transport):
+@pytest.mark.parametrize("P,transport,halo,patch", [(2, "host", False, 16), (2, "p2p", False, 16),
+                                                    (3, "p2p", False, 16), (2, "p2p", True, 16),
+                                                    (3, "p2p", True, 16), (2, "p2p", True, 96)])
+def test_two_process_shards_match_single_world(tmp_path, P, transport, halo, patch):
     """Several processes on one GPU; "p2p" maps the other processes' buffers
-    through IPC and synchronises on device flags, as across GPUs."""
+    through IPC and synchronises on device flags, as across GPUs; halo=True
+    pushes only the bodies within a cell of each peer's bounds (96x96
+    patches: 36 push blocks per rank, a wave-aggregated inbox per peer)."""
     import torch.multiprocessing as mp
     import rbhip
     from rbhip import scenes
     steps = 80
-    sc = scenes.tiled(scenes.flat_spheres, P, 16, 16, seed=2)
+    sc = scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2)
     with rbhip.World(sc) as w:
         w.step(steps)
         q1, v1 = w.get_state()
     out = str(tmp_path / "state.npy")
-    mp.start_processes(_worker, args=(P, _free_port(), steps, out, transport), nprocs=P, start_method="spawn")
+    mp.start_processes(_worker, args=(P, _free_port(), steps, out, transport, halo, patch), nprocs=P,
+                       start_method="spawn")
     got = np.load(out)
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
 
@@ -132,7 +137,7 @@ def test_sharded_world_on_nccl_group_one_rank(tmp_path, transport, expect):
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
 
 
-def _timeout_worker(rank, P, port, out):
+def _timeout_worker(rank, P, port, out, halo=False):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -141,7 +146,7 @@ def _timeout_worker(rank, P, port, out):
     import rbhip
     from rbhip import scenes
     from rbhip.shard import ShardedWorld
-    sw = ShardedWorld(scenes.tiled(scenes.flat_spheres, P, 8, 8, seed=1), device=0, transport="p2p")
+    sw = ShardedWorld(scenes.tiled(scenes.flat_spheres, P, 8, 8, seed=1), device=0, transport="p2p", halo=halo)
     msg = "no error"
     if rank == 0:                      # rank 1 never steps: rank 0's exchange must give up, not hang
         sw.step(4)
@@ -155,12 +160,13 @@ def _timeout_worker(rank, P, port, out):
     dist.destroy_process_group()
 
 
-def test_p2p_exchange_times_out_instead_of_hanging(tmp_path):
+@pytest.mark.parametrize("halo", [False, True])
+def test_p2p_exchange_times_out_instead_of_hanging(tmp_path, halo):
     import time
     import torch.multiprocessing as mp
     out = str(tmp_path / "msg.txt")
     t0 = time.time()
-    mp.start_processes(_timeout_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    mp.start_processes(_timeout_worker, args=(2, _free_port(), out, halo), nprocs=2, start_method="spawn")
     msg = open(out).read()
     assert "exchange timed out" in msg, msg
     assert time.time() - t0 < 60
