@@ -75,7 +75,7 @@ typedef struct rb_scene_desc {
     int32_t rank;              /* shard index: owns bodies [rank*S, rank*S+S) ∩ [0,N)  */
     int32_t world_size;        /* shard count P; S = ceil(N / P)                       */
     int32_t max_partners;      /* sphere-sphere contacts per body (0 = default 16)     */
-    int32_t bucket_capacity;   /* reserved: broadphase ids per cell bucket are 32      */
+    int32_t bucket_capacity;   /* reserved (0): a broadphase bucket holds 30 ids       */
     const int32_t *kind;       /* [N]   RB_BODY_*                                      */
     const double  *mass;       /* [N]   model.body_mass of each free body              */
     const double  *inertia;    /* [N*3] model.body_inertia (principal, body frame)     */

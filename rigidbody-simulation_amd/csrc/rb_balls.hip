@@ -94,7 +94,7 @@ template <typename T> __device__ __forceinline__ bool ball_hit(V3<T> pa, T ra, V
 }
 
 template <typename T, int MAXP>
-__device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int tid, int32_t *s_id) {
+__device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int tid, int32_t *s_id, uint32_t gen) {
     const int32_t i = p.lo + l;
     const Snap<T> own = p.snap_cur[i];            // post-ground position, radius
     const Vel<T> ov = p.vel_cur[i];
@@ -104,7 +104,7 @@ __device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int
     const M3<T> Ii = ball_iinv(mi, ri);
 
     // pairs: every partner within reach on the post-ground positions
-    const int32_t np_ = search_buckets<T, MAXP>(p, i, xo, s_id, tid, [&](uint32_t tj, const Snap<T> &s) {
+    const int32_t np_ = search_buckets<T, MAXP>(p, i, xo, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
         const int32_t j = (int32_t)(tj & ~BOX_FLAG);
         if (j == i) return false;
         const V3<T> xj = {s.x, s.y, s.z};
@@ -170,7 +170,7 @@ __device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int
     Snap<T> sn;
     sn.x = x.x; sn.y = x.y; sn.z = x.z; sn.r = ri;
     Claim cl{0u, -1};
-    if (p.next.cnt) cl = claim_slot(p.grid, p.next, p.err, sn);
+    if (p.next.line) cl = claim_slot(p.grid, p.next, p.err, sn, gen + 1u);
     wt_store(p.snap_next + i, sn);
     Vel<T> vn;
     vn.vx = v.x; vn.vy = v.y; vn.vz = v.z; vn.wx = w.x; vn.wy = w.y; vn.wz = w.z; vn.pad0 = T(0); vn.pad1 = T(0);
@@ -183,9 +183,10 @@ __global__ __launch_bounds__(STEP_BLOCK) void ball_step_kernel(StepParams<T> p) 
     __shared__ int32_t s_id[MAXP * STEP_BLOCK];
     const int tid = threadIdx.x;
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
-    if (gt < p.n_local) ball_body<T, MAXP>(p, (int32_t)gt, tid, s_id);
-    // counts of the table two steps ahead, last (see step_body)
-    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
+    // generations: see step_body
+    const uint32_t gen = *p.cur.gen;
+    if (p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
+    if (gt < p.n_local) ball_body<T, MAXP>(p, (int32_t)gt, tid, s_id, gen);
 }
 
 // Ground phase of the coming step from the true state: post-ground snapshot

@@ -2,11 +2,12 @@
 //
 // A world owns its device buffers — struct-of-arrays state, replicated
 // constants, two ping-pong position snapshots (which double as the
-// replicated exchange buffer of sharded worlds) and three rotating
-// broadphase tables — and enqueues all work on one HIP stream.  A step's
-// buffers are fixed by the step counter modulo 6 (tables mod 3, snapshots
-// mod 2), so multi-step calls on a single shard are captured once per
-// phase into a hipGraph (one kernel node per step) and replayed.
+// replicated exchange buffer of sharded worlds) and two alternating
+// broadphase tables (generation-tagged bucket lines, never cleared) — and
+// enqueues all work on one HIP stream.  A step's buffers are fixed by the
+// step counter's parity (and table generations live on the device), so
+// multi-step calls are captured once per parity into a hipGraph (one kernel
+// node per step) and replayed.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>   // types only: RCCL is dlopen'ed by the sharded path
@@ -62,7 +63,7 @@ int err_to_code(int32_t bits) {
     if (bits & ERR_UNSUPPORTED)
         return fail(RB_EUNSUPPORTED, "device: box-box / box-sphere pair within contact range (not restated)");
     if (bits & ERR_PARTNER_OVERFLOW) return fail(RB_EOVERFLOW, "device: a body has more sphere partners than max_partners");
-    if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: more than 32 bodies hashed to one broadphase cell");
+    if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: more than 30 bodies hashed to one broadphase bucket");
     return RB_OK;
 }
 
@@ -93,9 +94,10 @@ struct rb_world {
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
-    int32_t *cnt[3] = {};      // [H] broadphase bucket counts (rotate mod 3)
-    uint32_t *ids[2] = {};     // [H][BUCKET_SLOTS] bucket slot ids (alternate with the snapshots)
-    void *pos[2] = {};         // [H][BUCKET_SLOTS] Snap<T> bucket slot snapshots
+    uint32_t *ids[2] = {};     // [H][LINE_WORDS] bucket lines: header + ids (alternate with the snapshots)
+    void *pos[2] = {};         // [H][LINE_WORDS] Snap<T> bucket slot snapshots
+    uint32_t *gen = nullptr;   // [2] generation of the table of each step parity (rb_internal.hpp Table)
+    uint32_t gen_off = 1;      // generation of step c's table = gen_off + c (host bookkeeping; only grows)
     int32_t *plist = nullptr;      // split form: [MAXP][S] sorted partner ids
     int32_t *plist_cnt = nullptr;  // split form: [S] partner counts
     int32_t *err = nullptr;
@@ -127,7 +129,6 @@ struct rb_world {
     double t_sum_ms = 0;
     int64_t t_n = 0;
 
-    int phase() const { return (int)(c % 3); }
     int sp() const { return (int)(c % 2); }
 };
 
@@ -144,9 +145,9 @@ template <typename T> Grid<T> make_grid(const rb_world *w) {
     return g;
 }
 
-// the broadphase of the step whose counts are cnt[ph] and slots [sp]
-template <typename T> Table<T> table(const rb_world *w, int ph, int sp) {
-    return Table<T>{w->cnt[ph], w->ids[sp], w->pos[sp] ? dp<Snap<T>>(w->pos[sp], 0) : nullptr};
+// the broadphase of the steps of parity sp
+template <typename T> Table<T> table(const rb_world *w, int sp) {
+    return Table<T>{w->ids[sp], w->pos[sp] ? dp<Snap<T>>(w->pos[sp], 0) : nullptr, w->gen + sp};
 }
 
 // parameters of the step with counter value c
@@ -170,12 +171,11 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.dt = (T)dt; p.e = (T)e; p.mu = (T)mu; p.thr = (T)thr;
     p.oriented = w->oriented;
     p.grid = make_grid<T>(w);
-    const int ph = (int)(c % 3), sp = (int)(c % 2);
+    const int sp = (int)(c % 2);
     p.snap_cur = dp<Snap<T>>(w->snap[sp], 0);
     p.snap_next = dp<Snap<T>>(w->snap[1 - sp], 0);
-    p.cur = table<T>(w, ph, sp);
-    p.next = insert_next ? table<T>(w, (ph + 1) % 3, 1 - sp) : Table<T>{nullptr, nullptr, nullptr};
-    p.cnt_clear = w->cnt[(ph + 2) % 3];
+    p.cur = table<T>(w, sp);
+    p.next = insert_next ? table<T>(w, 1 - sp) : Table<T>{nullptr, nullptr, nullptr};
     p.err = w->err;
     p.epoch = w->p2p ? w->epoch : nullptr;
     p.bounds = w->halo ? w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE : nullptr;
@@ -195,14 +195,14 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     return p;
 }
 
-template <typename T> InsertParams<T> make_insert(rb_world *w, int sp, int ph, int64_t first, int64_t count,
+template <typename T> InsertParams<T> make_insert(rb_world *w, int sp, int64_t first, int64_t count,
                                                   int64_t skip_lo, int64_t skip_hi) {
     InsertParams<T> ip{};
     ip.snap = dp<Snap<T>>(w->snap[sp], 0);
     ip.kind = w->kind;
     ip.first = first; ip.count = count; ip.skip_lo = skip_lo; ip.skip_hi = skip_hi;
     ip.grid = make_grid<T>(w);
-    ip.tab = table<T>(w, ph, sp);
+    ip.tab = table<T>(w, sp);
     ip.err = w->err;
     return ip;
 }
@@ -227,10 +227,12 @@ int prime(rb_world *w, double dt = 0, double e = 0, double mu = 0) {
         HIPCHK(r);
         w->prm_dt = dt; w->prm_e = e; w->prm_mu = mu;
     }
-    for (int k = 0; k < 3; ++k) HIPCHK(hipMemsetAsync(w->cnt[k], 0, sizeof(int32_t) * w->H, w->stream));
+    // a fresh table: a generation above every one used so far
+    w->gen_off += 1;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(w->gen + w->sp()), (int)(w->gen_off + (uint32_t)w->c), 1, w->stream));
     hipError_t ie = w->dtype == RB_F64
-                        ? launch_insert<double>(make_insert<double>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream)
-                        : launch_insert<float>(make_insert<float>(w, w->sp(), w->phase(), 0, w->N, 0, 0), w->stream);
+                        ? launch_insert<double>(make_insert<double>(w, w->sp(), 0, w->N, 0, 0), w->stream)
+                        : launch_insert<float>(make_insert<float>(w, w->sp(), 0, w->N, 0, 0), w->stream);
     HIPCHK(ie);
     w->primed = true;
     return RB_OK;
@@ -317,10 +319,10 @@ Rccl &rccl() {
     return r;
 }
 
-// the peer-to-peer exchange of the next snapshot (parity nsp, table nph)
-template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp, int nph) {
+// the peer-to-peer exchange of the next snapshot and table (parity nsp)
+template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp) {
     P2PParams<T> pp{};
-    pp.ins = make_insert<T>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local);
+    pp.ins = make_insert<T>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local);
     pp.dst = dp<Snap<T>>(w->snap[nsp], 0);
     pp.peer_snap = reinterpret_cast<const Snap<T> *const *>(w->peer_snap_dev + (size_t)nsp * w->P);
     pp.peer_flags = w->peer_flags_dev;
@@ -333,10 +335,10 @@ template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp, int nph) {
     return pp;
 }
 
-// the halo exchange after the step kernel of step c (next snapshot nsp, table nph)
-template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp, int nph) {
+// the halo exchange after the step kernel of step c (next snapshot and table nsp)
+template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
     HaloParams<T> hp{};
-    hp.ins = make_insert<T>(w, nsp, nph, 0, 0, 0, 0);
+    hp.ins = make_insert<T>(w, nsp, 0, 0, 0, 0);
     hp.dst = dp<Snap<T>>(w->snap[nsp], 0);
     hp.bounds = w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE;
     hp.bounds_reset = w->bounds + ((c + 1) % 2) * BOUND_COPIES * BOUND_STRIDE;
@@ -359,20 +361,20 @@ template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp, i
 // in-place all-gather of that snapshot, then the insert of every other
 // rank's bodies into the next table (as rb_shard_exchange_done).
 int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
-    const int nsp = 1 - (int)(c % 2), nph = (int)((c + 1) % 3);
+    const int nsp = 1 - (int)(c % 2);
     if (w->p2p && w->halo) {
-        const hipError_t he = w->dtype == RB_F64 ? launch_halo_exchange<double>(make_halo<double>(w, c, nsp, nph), s)
-                                                 : launch_halo_exchange<float>(make_halo<float>(w, c, nsp, nph), s);
+        const hipError_t he = w->dtype == RB_F64 ? launch_halo_exchange<double>(make_halo<double>(w, c, nsp), s)
+                                                 : launch_halo_exchange<float>(make_halo<float>(w, c, nsp), s);
         HIPCHK(he);
         return RB_OK;
     }
     if (w->p2p) {
         hipError_t pe;
         if (w->dtype == RB_F64) {
-            P2PParams<double> pp = make_p2p<double>(w, nsp, nph);
+            P2PParams<double> pp = make_p2p<double>(w, nsp);
             pe = launch_p2p_exchange<double>(pp, s);
         } else {
-            P2PParams<float> pp = make_p2p<float>(w, nsp, nph);
+            P2PParams<float> pp = make_p2p<float>(w, nsp);
             pe = launch_p2p_exchange<float>(pp, s);
         }
         HIPCHK(pe);
@@ -385,8 +387,8 @@ int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
     if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
     const hipError_t ie =
         w->dtype == RB_F64
-            ? launch_insert<double>(make_insert<double>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), s)
-            : launch_insert<float>(make_insert<float>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), s);
+            ? launch_insert<double>(make_insert<double>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local), s)
+            : launch_insert<float>(make_insert<float>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local), s);
     HIPCHK(ie);
     return RB_OK;
 }
@@ -401,6 +403,21 @@ void drop_graphs(rb_world *w) {
     w->graphs.clear();
 }
 
+// Table generations are 32-bit and only grow: before they would wrap (after
+// ~4e9 steps of one world) the bucket lines are zeroed and the table
+// rebuilt at generation 2 — from the snapshot, which holds every body's
+// position except in a halo-exchanging shard (there: an error).
+int gen_guard(rb_world *w, int64_t nsteps) {
+    const uint64_t g = (uint32_t)(w->gen_off + (uint32_t)w->c);
+    if (g + (uint64_t)nsteps + 4 < (1ull << 32)) return RB_OK;
+    if (w->halo) return fail(RB_EOVERFLOW, "table generations exhausted: call rb_set_state to restart the halo exchange");
+    HIPCHK(hipStreamSynchronize(w->stream));
+    for (int k = 0; k < 2; ++k) HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
+    w->gen_off = 1u - (uint32_t)w->c;   // prime() makes step c's generation 2
+    w->primed = false;
+    return RB_OK;
+}
+
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
@@ -411,6 +428,7 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
     HIPCHK(hipSetDevice(w->device));
+    if (int rc = gen_guard(w, nsteps)) return rc;
     if (!w->primed || (w->law == RB_LAW_BALLS && (dt != w->prm_dt || e != w->prm_e || mu != w->prm_mu))) {
         int rc = prime(w, dt, e, mu);
         if (rc) return rc;
@@ -440,13 +458,13 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     int64_t left = nsteps;
     while (left > 0) {
         const int64_t K = left > chunk_max ? chunk_max : left;
-        auto key = std::make_tuple(K, (int)(w->c % 6), dt, e, mu, thr, variant);
+        auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
         auto it = w->graphs.find(key);
         if (it == w->graphs.end()) {
             if (w->graphs.size() >= 60) drop_graphs(w);
-            // capture the six buffer-phase variants at once, so later calls
-            // starting at any phase replay without a capture
-            for (int c0 = 0; c0 < 6; ++c0) {
+            // capture both parities at once, so later calls starting at
+            // either replay without a capture
+            for (int c0 = 0; c0 < 2; ++c0) {
                 hipGraph_t graph;
                 hipGraphExec_t ex;
                 HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
@@ -554,7 +572,7 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->cnt[0], w->cnt[1], w->cnt[2],
+    void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->gen,
                     w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
@@ -642,7 +660,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     ALLOC(w->state, (size_t)w->esz * 13 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
-    for (int k = 0; k < 3; ++k) ALLOC(w->cnt[k], sizeof(int32_t) * w->H);
+    ALLOC(w->gen, sizeof(uint32_t) * 2);
     // Experimental, opt-in (RBHIP_SPLIT=1): large scenes step in two kernels
     // (search, update) joined by a partner list.  Not yet validated on the
     // device; the default is the fused one-kernel step.
@@ -654,9 +672,9 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         ALLOC(w->plist_cnt, sizeof(int32_t) * w->S);
     }
     for (int k = 0; k < 2; ++k) {
-        ALLOC(w->ids[k], sizeof(uint32_t) * BUCKET_SLOTS * w->H);
+        ALLOC(w->ids[k], sizeof(uint32_t) * LINE_WORDS * w->H);
         // slot snapshots feed the cooperative search only
-        if (needs_slot_snapshots(coop, split)) ALLOC(w->pos[k], (size_t)w->esz * 4 * BUCKET_SLOTS * w->H);
+        if (needs_slot_snapshots(coop, split)) ALLOC(w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H);
     }
     ALLOC(w->err, sizeof(int32_t));
 #undef ALLOC
@@ -668,6 +686,10 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (hipMemset(w->snap[0], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
         hipMemset(w->snap[1], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
         hipMemset(w->state, 0, (size_t)w->esz * 13 * w->S) != hipSuccess ||
+        // bucket headers of generation 0: every table's generation is >= 2
+        hipMemset(w->ids[0], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
+        hipMemset(w->ids[1], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
+        hipMemset(w->gen, 0, sizeof(uint32_t) * 2) != hipSuccess ||
         hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipMemset failed"));
     std::vector<double> bound;
@@ -748,6 +770,7 @@ int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
     if (w->law != RB_LAW_MUJOCO) return fail(RB_EUNSUPPORTED, "sharded stepping supports the default contact law only");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0)) return fail(RB_EINVAL, "invalid step parameters");
     HIPCHK(hipSetDevice(w->device));
+    if (int rc = gen_guard(w, 1)) return rc;
     if (!w->primed) { int rc = prime(w); if (rc) return rc; }
     if (w->timing) return timed_launch(w, dt, e, mu, thr);
     return launch_one(w, w->stream, w->c, dt, e, mu, thr);
@@ -758,10 +781,10 @@ int rb_shard_exchange_done(rb_world *w) {
     HIPCHK(hipSetDevice(w->device));
     // insert every body not owned here into the next table (own ones went in
     // from the step kernel), reading the freshly exchanged snapshot
-    const int nsp = 1 - w->sp(), nph = (w->phase() + 1) % 3;
+    const int nsp = 1 - w->sp();
     hipError_t e = w->dtype == RB_F64
-                       ? launch_insert<double>(make_insert<double>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream)
-                       : launch_insert<float>(make_insert<float>(w, nsp, nph, 0, w->N, w->lo, w->lo + w->n_local), w->stream);
+                       ? launch_insert<double>(make_insert<double>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local), w->stream)
+                       : launch_insert<float>(make_insert<float>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local), w->stream);
     HIPCHK(e);
     ++w->c;
     return RB_OK;

@@ -108,44 +108,53 @@ __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, in
     return true;
 }
 
-// Append a body (tagged id + snapshot) to the bucket of its cell: one
-// returning atomicAdd claims the slot (claim_slot), the slot is then
-// written (publish_slot).  Split so a caller can put independent work
-// between the two and hide the atomic's round trip.
+// Append a body (tagged id + snapshot) to the bucket of its cell in the
+// table of generation gen (rb_internal.hpp Table): an atomicMax raises a
+// stale header to (gen, 0), a returning atomicAdd claims the slot
+// (claim_slot); the slot is then written (publish_slot).  Split so a caller
+// can put independent work between the two and hide the atomic's round trip.
 struct Claim { uint32_t b; int32_t slot; };      // slot < 0: not inserted
 template <typename T>
-__device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn) {
+__device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
+                                            uint32_t gen) {
     int32_t ix, iy, iz;
     if (!cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return {0u, -1}; }
     const uint32_t b = bucket_of(ix, iy, iz, g);
-    return {b, atomicAdd(tab.cnt + b, 1)};
+    auto *h = reinterpret_cast<unsigned long long *>(tab.line + (int64_t)CHK(b, g.H) * LINE_WORDS);
+    atomicMax(h, (unsigned long long)gen << 32);
+    const unsigned long long old = atomicAdd(h, 1ull);
+    // after the max the header carries gen (no later generation writes this
+    // table before the next step's launch)
+    const int32_t slot = (uint32_t)(old >> 32) == gen ? (int32_t)(uint32_t)old : BUCKET_SLOTS;
+    return {b, slot};
 }
 template <typename T>
 __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
                                              uint32_t tagged_id) {
     if (c.slot < 0) return;
     if (c.slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    const int64_t o = CHK((int64_t)c.b * BUCKET_SLOTS + c.slot, RB_BOUNDS ? 1ll << 40 : 0);
-    wt_store(tab.ids + o, tagged_id);
-    if (tab.pos) wt_store(tab.pos + o, sn);
+    const int64_t o = CHK((int64_t)c.b * LINE_WORDS + HEAD_WORDS + c.slot, RB_BOUNDS ? 1ll << 40 : 0);
+    wt_store(tab.line + o, tagged_id);
+    if (tab.pos) wt_store(tab.pos + (int64_t)c.b * LINE_WORDS + c.slot, sn);
 }
 template <typename T>
 __device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
-                                          uint32_t tagged_id) {
-    publish_slot(tab, err, claim_slot(g, tab, err, sn), sn, tagged_id);
+                                          uint32_t tagged_id, uint32_t gen) {
+    publish_slot(tab, err, claim_slot(g, tab, err, sn, gen), sn, tagged_id);
 }
 
-// count (clamped) and the first 4 ids of a bucket, loaded together
+// A bucket's header and first two ids in one 16-byte load; count = 0 unless
+// the header carries the table's generation (clamped to the slots).
 template <typename T>
-__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int32_t &count) {
-    const int32_t c = tab.cnt[CHK(b, RB_BOUNDS ? 1ll << 40 : 0)];
-    const uint4 h = *reinterpret_cast<const uint4 *>(tab.ids + (int64_t)b * BUCKET_SLOTS);
-    count = c < BUCKET_SLOTS ? c : BUCKET_SLOTS;
-    return h;
+__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b) {
+    return *reinterpret_cast<const uint4 *>(tab.line + (int64_t)CHK(b, RB_BOUNDS ? 1ll << 40 : 0) * LINE_WORDS);
+}
+__device__ __forceinline__ int32_t head_count(const uint4 &h, uint32_t gen) {
+    return h.y != gen ? 0 : h.x < (uint32_t)BUCKET_SLOTS ? (int32_t)h.x : BUCKET_SLOTS;
 }
 template <typename T>
 __device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s) {
-    return s == 0 ? h.x : s == 1 ? h.y : s == 2 ? h.z : s == 3 ? h.w : tab.ids[(int64_t)b * BUCKET_SLOTS + s];
+    return s == 0 ? h.z : s == 1 ? h.w : tab.line[(int64_t)b * LINE_WORDS + HEAD_WORDS + s];
 }
 
 // The 2x2x2 cell neighbourhood: cell size = 2 x the largest contact reach
@@ -178,29 +187,29 @@ __device__ __forceinline__ void list_insert(int32_t *s_id, int stride, int slot,
     ++np_;
 }
 
-// One lane per body: the 8 bucket counts and the first 4 ids of each bucket
-// are loaded together, then candidates in batches of RB_QBATCH (snapshot
+// One lane per body: the 8 bucket heads (count and first 2 ids) are loaded
+// together, then candidates in batches of RB_QBATCH (snapshot
 // loads in flight together); hit(tagged id, snapshot) decides a partner.
 // The partners go to the body's LDS column of s_id in ascending id order.
 // Returns the partner count.
 template <typename T, int MAXP, typename Hit>
 __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
-                                                  int tid, Hit hit) {
+                                                  int tid, uint32_t gen, Hit hit) {
     constexpr int NB = STEP_BLOCK;
     int32_t cx, cy, cz, sx, sy, sz;
     if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) { atomicOr(p.err, ERR_DOMAIN); return 0; }
     uint32_t b[8];
     int32_t c[8];
-    uint4 id4[8];
+    uint4 hd[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
         b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) id4[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H), c[k]);
+    for (int k = 0; k < 8; ++k) hd[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H));
     int32_t total = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        int32_t n = c[k];
+        int32_t n = head_count(hd[k], gen);
 #pragma unroll
         for (int j = 0; j < k; ++j)
             if (b[j] == b[k]) n = 0;                  // two cells hashed to one bucket: visit once
@@ -225,15 +234,13 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (rem >= 0 && rem < c[k]) {
-                    if (rem == 0) t = id4[k].x;
-                    else if (rem == 1) t = id4[k].y;
-                    else if (rem == 2) t = id4[k].z;
-                    else if (rem == 3) t = id4[k].w;
-                    else addr = (int64_t)b[k] * BUCKET_SLOTS + rem;
+                    if (rem == 0) t = hd[k].z;
+                    else if (rem == 1) t = hd[k].w;
+                    else addr = (int64_t)b[k] * LINE_WORDS + HEAD_WORDS + rem;
                 }
                 rem -= c[k];
             }
-            if (base + u < total && addr >= 0) t = p.cur.ids[CHK(addr, (int64_t)p.grid.H * BUCKET_SLOTS)];
+            if (base + u < total && addr >= 0) t = p.cur.line[CHK(addr, (int64_t)p.grid.H * LINE_WORDS)];
             tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
         // the id-indexed snapshot: ids are spatially coherent, so a wave's

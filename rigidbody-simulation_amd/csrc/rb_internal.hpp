@@ -26,19 +26,29 @@ enum : int32_t {
 // layout [P][S][4], rank r's bodies are the contiguous slice [r*S, r*S+S).
 template <typename T> struct alignas(4 * sizeof(T)) Snap { T x, y, z, r; };
 
-// Broadphase buckets: per-cell hash -> a count, a 128-byte line of body ids
-// and, slot for slot, the bodies' snapshots, so a query reads candidates'
-// positions from the bucket it already holds instead of chasing ids into
-// the id-indexed snapshot.  A body claims its slot with one atomicAdd on the
-// count; counts are cleared two steps ahead by the step kernel's grid
-// (three count arrays rotate), slots are overwritten (two slot arrays
-// alternate with the snapshots).
-constexpr int BUCKET_SLOTS = 32;
+// Broadphase buckets: per-cell hash -> one 128-byte line holding an 8-byte
+// header and 30 body ids, and (cooperative search) slot for slot the
+// bodies' snapshots, so a query reads candidates' positions from the bucket
+// it already holds instead of chasing ids into the id-indexed snapshot.
+//
+// The header is (generation << 32) | count.  Every table (the one a step
+// reads, the one it fills for the next step) has a generation number that
+// only grows; a header with an older generation is an empty bucket.  So a
+// query reads count and first two ids with ONE 16-byte load, and nothing is
+// ever cleared: an inserter first raises a stale header to (generation, 0)
+// with a 64-bit atomicMax, then claims its slot with a 64-bit atomicAdd (two
+// atomics of one thread on one address stay in order).  Two line arrays
+// alternate with the snapshots.  The generation of the table a step reads
+// sits in device memory (gen[step parity]); the step kernel writes the next
+// one, so graph replays need no host input.
+constexpr int LINE_WORDS = 32;               // uint32 words per bucket line
+constexpr int HEAD_WORDS = 2;                // the header's words
+constexpr int BUCKET_SLOTS = LINE_WORDS - HEAD_WORDS;
 constexpr uint32_t BOX_FLAG = 0x80000000u;   // set on ids of box bodies
 template <typename T> struct Table {
-    int32_t *cnt;              // [H]
-    uint32_t *ids;             // [H][BUCKET_SLOTS]
-    Snap<T> *pos;              // [H][BUCKET_SLOTS]; nullptr: not kept (one-lane search)
+    uint32_t *line;            // [H][LINE_WORDS]: header, then ids
+    Snap<T> *pos;              // [H][LINE_WORDS] slot snapshots (slot s at s); nullptr: not kept
+    uint32_t *gen;             // this table's generation (device word)
 };
 
 constexpr int MAX_PLANES = 8;
@@ -110,8 +120,7 @@ template <typename T> struct StepParams {
     Grid<T> grid;
     Snap<T> *snap_next;                // next step's snapshot (own rows written)
     Table<T> cur;                      // broadphase of snap_cur
-    Table<T> next;                     // broadphase of snap_next (own ids inserted); cnt == nullptr: skip
-    int32_t *cnt_clear;                // counts of the table two steps ahead
+    Table<T> next;                     // broadphase of snap_next (own ids inserted); line == nullptr: skip
     int32_t *err;
     int64_t *epoch;                    // peer-to-peer exchange: step count, advanced by block 0 (else nullptr)
     int32_t *bounds;                   // halo exchange: [BOUND_COPIES][BOUND_STRIDE] cell bounds of the

@@ -16,8 +16,8 @@
 //      (collision.py:90-95): state written in place, the new position into
 //      the next snapshot;
 //   and the next step's broadphase: the body inserts its id into the next
-//   table while the grid clears the counts of the table two steps ahead.
-//   Three tables and two snapshots rotate, so a step reads only data no
+//   table (a newer generation, rb_internal.hpp Table: nothing is cleared).
+//   Two tables and two snapshots alternate, so a step reads only data no
 //   thread of the same launch writes: Jacobi across bodies, exactly as
 //   multi_sphere_bounce.py:43-46 (one mj_forward per step).
 #include "rb_device.hpp"
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
     if (k >= p.count) return;
     const int64_t id = p.first + k;
     if (id >= p.skip_lo && id < p.skip_hi) return;
-    insert_id(p.grid, p.tab, p.err, p.snap[id], (uint32_t)id | (p.kind[id] != 0 ? BOX_FLAG : 0u));
+    insert_id(p.grid, p.tab, p.err, p.snap[id], (uint32_t)id | (p.kind[id] != 0 ? BOX_FLAG : 0u), *p.tab.gen);
 }
 
 template <typename T>
@@ -127,14 +127,14 @@ __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i,
 // candidate test).
 template <typename T, int MAXP>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
-                                                   T rad, T bi, int32_t *s_id, int tid) {
-    return search_buckets<T, MAXP>(p, i, x, s_id, tid, [&](uint32_t tj, const Snap<T> &s) {
+                                                   T rad, T bi, int32_t *s_id, int tid, uint32_t gen) {
+    return search_buckets<T, MAXP>(p, i, x, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
         return candidate_hit(p, i, kind, x, rad, bi, tj, s);
     });
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
-// cell k.  Its count, first ids and first RB_QSPEC slot snapshots are
+// cell k.  Its header (count, first 2 ids) and first RB_QSPEC slot snapshots are
 // loaded together (slots past the count are stale and ignored), and while
 // they are in flight the lane evaluates the body's inverse world inertia
 // (pre, if PRE).  Hits become a bitmask over the bucket slots; a group prefix sum
@@ -144,7 +144,8 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
 template <typename T, int MAXP, int G, typename Overlap>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
                                                V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
-                                               Snap<T> *t_pos, int slot, int k, int lane, Overlap overlap) {
+                                               Snap<T> *t_pos, int slot, int k, int lane, uint32_t gen,
+                                               Overlap overlap) {
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
     constexpr int QB = RB_QBATCH;
@@ -157,19 +158,18 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     }
     const uint32_t b = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0),
                                  p.grid);
-    const int64_t base = (int64_t)b * BUCKET_SLOTS;
+    const int64_t base = (int64_t)b * LINE_WORDS;      // slot snapshots: slot s at base + s
     [[maybe_unused]] const int tid = lane;   // STAMP
     STAMP(8);
     // loaded unconditionally (b is a valid bucket for every lane) and the
     // count clamped only after overlap(): a use inside a branch would make
     // the wave wait for the loads before that work starts
-    const int32_t craw = p.cur.cnt[b];
-    const uint4 id4 = *reinterpret_cast<const uint4 *>(p.cur.ids + base);
+    const uint4 id4 = bucket_head(p.cur, b);
     Snap<T> p4[QS];
 #pragma unroll
     for (int u = 0; u < QS; ++u) p4[u] = p.cur.pos[base + u];
     overlap();                                    // body work under the bucket loads
-    int32_t c = !ok ? 0 : craw < BUCKET_SLOTS ? craw : BUCKET_SLOTS;
+    int32_t c = !ok ? 0 : head_count(id4, gen);
     STAMP(9);
     const int gbase = lane & ~(G - 1);
 #pragma unroll
@@ -280,7 +280,7 @@ template <typename T, bool POS>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, bool forced, LazyInvI<T> &invI,
                                             int32_t np_, const int32_t *pid, int64_t stride, const Snap<T> *ppos,
-                                            int tid, int32_t *cell) {
+                                            int tid, int32_t *cell, uint32_t gen_next) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -363,7 +363,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // atomic would wait for every older store), its round trip overlaps the
     // snapshot store and the quaternion update
     Claim cl{0u, -1};
-    if (p.next.cnt) cl = claim_slot(p.grid, p.next, p.err, sn);
+    if (p.next.line) cl = claim_slot(p.grid, p.next, p.err, sn, gen_next);
     wt_store(p.snap_next + i, sn);
     if (p.bounds) {                              // halo exchange: this body's new cell
         int32_t cx, cy, cz;
@@ -387,7 +387,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 template <typename T, int MAXP, int G>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
-                                          int32_t *cell) {
+                                          int32_t *cell, uint32_t gen) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = p.lo + l;
@@ -412,11 +412,11 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     STAMP(1);
     int32_t np_ = 0;
     if constexpr (G == 1) {
-        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid);
+        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid, gen);
     } else {
         if (RB_ABLATE != 1)
             np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                          [&] {
+                                          gen, [&] {
                                               invI.get();
                                               if (!p.xfrc) {
                                                   apply_force(p, l, in.m, invI, in.v, in.w);
@@ -432,7 +432,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
         invI.q = in.q;
     }
     body_update<T, (G > 1)>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB, s_pos + slot, tid,
-                            cell);
+                            cell, gen + 1u);
 }
 
 // Halo exchange: fold the wave's new cells (cell[0] == INT32_MAX: none) into
@@ -468,7 +468,6 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
     const int tid = threadIdx.x;
-    const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
     if (RB_ABLATE == 3) return;
     STAMP(0);
     // one scalar round trip for the prologue's kernel arguments (the
@@ -477,17 +476,17 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
                  "s"(p.n_local), "s"(p.lo));
 
     if (p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;   // peer-to-peer exchange: this step's number
+    // generation of the table this step reads; the next table's is one more
+    // (published by block 0 for the kernels that insert after this one)
+    const uint32_t gen = *p.cur.gen;
+    if (p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
 
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < p.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
-    if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, cell);
+    if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, cell, gen);
     if (p.bounds) fold_bounds(p.bounds, cell);
-    // The counts of step t+2's table were last read by step t-1: clear them
-    // for step t+1's inserts.  Last, since every load or atomic issued after
-    // a store waits for it (vmcnt counts in issue order).
-    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
 }
 
 // The two forms as separate kernels: the one-lane (large-scene) form may be
@@ -536,10 +535,11 @@ __global__ __launch_bounds__(STEP_BLOCK) void search_kernel(StepParams<T> p) {
     const V3<T> x = {self.x, self.y, self.z};
     const int32_t kind = p.cs.kind[i];
     const T rad = p.cs.sx()[i];
+    const uint32_t gen = *p.cur.gen;
     int32_t np_;
-    if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, rad, self.r, s_id, tid);
+    if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, rad, self.r, s_id, tid, gen);
     else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                       [] {});
+                                       gen, [] {});
     if (!active) return;
     for (int s = k; s < np_; s += G) p.plist[CHK((int64_t)s * p.S + l, (int64_t)MAXP * p.S)] = s_id[s * NB + slot];
     if (k == 0) p.plist_cnt[CHK(l, p.S)] = np_;
@@ -551,6 +551,8 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
     const int64_t lb = gt;
     int32_t cell[3] = {INT32_MAX, 0, 0};
+    const uint32_t gen_next = *p.cur.gen + 1u;
+    if (p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen_next;
     if (lb < p.n_local) {
         const int32_t l = (int32_t)lb, i = p.lo + l;
         const Snap<T> self = p.snap_cur[CHK(i, p.n_global)];
@@ -564,10 +566,9 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
         const int32_t np_ = p.plist_cnt[CHK(l, p.S)];
         if (RB_BOUNDS && np_ > 16) printf("RB_BOUNDS np_ %d at l %d\n", np_, l);
         body_update<T, false>(p, l, i, x, kind, sz, self.r, in, false, invI, np_, p.plist + l, p.S, nullptr, tid,
-                              cell);
+                              cell, gen_next);
     }
     if (p.bounds) fold_bounds(p.bounds, cell);
-    for (int64_t h = gt; h < p.grid.H; h += (int64_t)gridDim.x * STEP_BLOCK) wt_store(p.cnt_clear + h, 0);
 }
 
 #if RB_STAMPS
@@ -632,7 +633,7 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, b
     const bool split = !coop && p.plist;
     // the cooperative search reads bucket slot snapshots: never launch it
     // on a table without them
-    if (needs_slot_snapshots(coop, split) && (!p.cur.pos || (p.next.cnt && !p.next.pos))) return hipErrorInvalidValue;
+    if (needs_slot_snapshots(coop, split) && (!p.cur.pos || (p.next.line && !p.next.pos))) return hipErrorInvalidValue;
     if (split) {
         constexpr int GS = SPLIT_SEARCH_LANES;
         const int64_t sblocks = blocks * GS;

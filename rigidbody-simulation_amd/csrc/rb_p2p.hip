@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
     if (id >= p.ins.count || (id >= p.ins.skip_lo && id < p.ins.skip_hi)) return;
     const Snap<T> s = p.peer_snap[id / p.S][id];
     p.dst[id] = s;
-    insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, (uint32_t)id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u));
+    insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, (uint32_t)id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u), *p.ins.tab.gen);
 }
 
 // ---- halo exchange (large shards) -----------------------------------------
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
     const int64_t total = s_off[p.P];
     const uint32_t *ids = reinterpret_cast<const uint32_t *>(p.mail + L.o_ids);
     const Snap<T> *sn = reinterpret_cast<const Snap<T> *>(p.mail + L.o_snap);
+    const uint32_t gen = *p.ins.tab.gen;
     for (int64_t k = (int64_t)blockIdx.x * 256 + tid; k < total; k += (int64_t)gridDim.x * 256) {
         int q = 0;
         while (k >= s_off[q + 1]) ++q;
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
             continue;
         }
         p.dst[id] = s;
-        insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u));
+        insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u), gen);
     }
 }
 

@@ -11,11 +11,22 @@ variants = os.environ.get("VARIANTS", "").split(";")
 envs = os.environ.get("ENVS", "").split(";")
 sizes = [tuple(int(v) for v in s.split("x")) for s in os.environ.get("SIZES", "64x64,256x256,1024x1024").split(",")]
 paths = {}
+# PREBUILT=1: use build/ablate<k>.so made beforehand (BUILD_ONLY=1 makes them
+# and exits), so the GPU box does not compile
+os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
 for k, v in enumerate(variants):
-    out = f"/tmp/librbhip_ablate{k}.so"
-    subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
-                   f"{v} -o {out} rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
+    out = os.path.join(ROOT, "build", f"ablate{k}.so")
+    if os.environ.get("PREBUILT") != "1":
+        subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
+                       f"{v} -o {out} rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True, check=True,
+                       cwd=CSRC)
     paths[v] = out
+if os.environ.get("BUILD_ONLY") == "1":
+    sys.exit(0)
+# LIBS: ";"-separated library paths to compare instead of VARIANTS builds
+if os.environ.get("LIBS"):
+    variants = os.environ["LIBS"].split(";")
+    paths = {v: os.path.join(ROOT, v) for v in variants}
 import torch  # noqa: E402  (initialise torch's HIP context before the library's)
 torch.cuda.init()
 from rbhip import _lib, scenes
