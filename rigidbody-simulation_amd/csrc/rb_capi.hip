@@ -76,6 +76,7 @@ struct rb_world {
     int32_t n_local = 0, P = 1, rank = 0;
     int32_t n_planes = 0, oriented = 1, maxp = 16, maxrec = 0;
     int64_t coop_max = 32768;   // owned bodies up to which the cooperative search is used
+    int64_t wide_max = 65536;   // above coop_max, up to which the wide one-lane form is used
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};
     double inv_cs = 1.0;
@@ -246,9 +247,9 @@ int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, doubl
         HIPCHK(r);
         return RB_OK;
     }
-    const bool coop = w->n_local <= w->coop_max;
-    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, coop, s);
-    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, coop, s);
+    const int form = w->n_local <= w->coop_max ? FORM_COOP : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
+    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, form, s);
+    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, form, s);
     HIPCHK(r);
     return RB_OK;
 }
@@ -636,6 +637,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxp = maxp;
     w->maxrec = 4 * w->n_planes + w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
+    if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     // per-cell hash: 16 buckets per body (occupied cells <= bodies), so few
     // cells share a bucket and few false candidates are read (measured: C3
     // +15% over 4 per body); at most 2^26 buckets (8 GB of id lines)

@@ -20,6 +20,15 @@
 #define RB_XCD_REMAP 0
 #endif
 
+// diagnostic builds (rb_kernels.hip lists them): 5 = no candidate snapshot
+// loads, 6 = no bucket loads for cells below z = 0
+#ifndef RB_ABLATE
+#define RB_ABLATE 0
+#endif
+// per-wave phase stamps (rb_kernels.hip RB_STAMPS builds)
+#ifndef STAMP
+#define STAMP(k) do {} while (0)
+#endif
 // candidates whose snapshot loads are issued together
 #ifndef RB_QBATCH
 #define RB_QBATCH 4
@@ -205,7 +214,11 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     for (int k = 0; k < 8; ++k)
         b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hd[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H));
+    for (int k = 0; k < 8; ++k) {
+        if (RB_ABLATE == 6 && (k & 4) && cz + sz < 0) hd[k] = uint4{0u, 0u, 0u, 0u};
+        else hd[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H));
+    }
+    STAMP(8);
     int32_t total = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -244,15 +257,126 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
             tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
         // the id-indexed snapshot: ids are spatially coherent, so a wave's
-        // candidates share lines (cheaper than bucket slots at this scale)
+        // candidates share lines (cheaper than bucket slots at this scale).
+        // The body itself (always in its own cell's bucket) and the padding
+        // of the last batch are no candidates: their lanes load nothing.
 #pragma unroll
-        for (int u = 0; u < RB_QBATCH; ++u) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+        for (int u = 0; u < RB_QBATCH; ++u) {
+            sn[u] = Snap<T>{RB_ABLATE == 5 ? x.x + T(1000) : x.x, x.y, x.z, T(0)};
+            if ((tj[u] & ~BOX_FLAG) != (uint32_t)i && RB_ABLATE != 5)
+                sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+        }
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u)
             if (hit(tj[u], sn[u]))
                 list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
         base += RB_QBATCH;
+        if (base == RB_QBATCH) STAMP(9);
     } while (base < total);
+    STAMP(10);
+    if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
+    return np_;
+}
+
+// ---- wide one-lane search (one wave per SIMD, rb_kernels.hip step_kernel_wide)
+// A bucket head of 32 bytes: header and the first WIDE_HEAD_IDS ids.
+constexpr int WIDE_HEAD_IDS = 6;
+constexpr int WIDE_QBATCH = 8;                      // candidates per round trip
+constexpr int WIDE_MAXC = 8 * WIDE_HEAD_IDS;        // head candidates listed in LDS
+struct Head6 { uint4 a, b; };
+template <typename T>
+__device__ __forceinline__ Head6 bucket_head6(const Table<T> &tab, uint32_t b) {
+    const uint4 *l = reinterpret_cast<const uint4 *>(tab.line + (int64_t)CHK(b, RB_BOUNDS ? 1ll << 40 : 0) * LINE_WORDS);
+    return Head6{l[0], l[1]};
+}
+template <int S> __device__ __forceinline__ uint32_t head6_id(const Head6 &h) {
+    static_assert(S >= 0 && S < WIDE_HEAD_IDS, "head slot");
+    return S == 0 ? h.a.z : S == 1 ? h.a.w : S == 2 ? h.b.x : S == 3 ? h.b.y : S == 4 ? h.b.z : h.b.w;
+}
+
+// The same contact set and order as search_buckets, with fewer dependent
+// round trips: the 8 heads carry 6 ids each, so candidates of the first 6
+// slots are known after the head round trip; they are listed (the body
+// itself left out) in the lane's LDS column s_cand and their snapshots
+// fetched WIDE_QBATCH at a time.  Slots past 6 (rare: a bucket of 7+
+// bodies) are read afterwards, ids then snapshots.  overlap() runs under
+// the head loads.  Meant for one wave per SIMD: it holds many registers.
+template <typename T, int MAXP, typename Hit, typename Overlap>
+__device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
+                                                       uint32_t *s_cand, int tid, uint32_t gen, Hit hit,
+                                                       Overlap overlap) {
+    constexpr int NB = STEP_BLOCK;
+    constexpr int QB = WIDE_QBATCH;
+    int32_t cx, cy, cz, sx, sy, sz;
+    if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) { atomicOr(p.err, ERR_DOMAIN); return 0; }
+    uint32_t b[8];
+    int32_t c[8];
+    Head6 hd[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hd[k] = bucket_head6(p.cur, (uint32_t)CHK(b[k], p.grid.H));
+    overlap();                                    // body work under the head loads
+    STAMP(8);
+    int32_t n = 0;
+    bool more = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int32_t m = head_count(hd[k].a, gen);
+#pragma unroll
+        for (int j = 0; j < k; ++j)
+            if (b[j] == b[k]) m = 0;                  // two cells hashed to one bucket: visit once
+        c[k] = m;
+        more |= m > WIDE_HEAD_IDS;
+#define RB_WIDE_LIST(S)                                                           \
+        if (S < m) {                                                              \
+            const uint32_t t = head6_id<S>(hd[k]);                                \
+            if ((t & ~BOX_FLAG) != (uint32_t)i) s_cand[n++ * NB + tid] = t;       \
+        }
+        RB_WIDE_LIST(0) RB_WIDE_LIST(1) RB_WIDE_LIST(2) RB_WIDE_LIST(3) RB_WIDE_LIST(4) RB_WIDE_LIST(5)
+#undef RB_WIDE_LIST
+    }
+    int32_t np_ = 0;
+    bool overflow = false;
+    for (int base = 0; base < n; base += QB) {
+        uint32_t tj[QB];
+        Snap<T> sn[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) tj[u] = base + u < n ? s_cand[(base + u) * NB + tid] : (uint32_t)i;
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+            sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
+            if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+        }
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+            if (base + u < n && hit(tj[u], sn[u])) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
+    }
+    STAMP(9);
+    if (more) {
+        // buckets of 7+ bodies: the remaining ids from their lines, QB at a time
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            for (int s0 = WIDE_HEAD_IDS; s0 < c[k]; s0 += QB) {
+                uint32_t tj[QB];
+                Snap<T> sn[QB];
+#pragma unroll
+                for (int u = 0; u < QB; ++u)
+                    tj[u] = s0 + u < c[k] ? p.cur.line[(int64_t)b[k] * LINE_WORDS + HEAD_WORDS + s0 + u] : (uint32_t)i;
+#pragma unroll
+                for (int u = 0; u < QB; ++u) {
+                    sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
+                    if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+                }
+#pragma unroll
+                for (int u = 0; u < QB; ++u)
+                    if (s0 + u < c[k] && hit(tj[u], sn[u]))
+                        list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
+            }
+        }
+    }
+    STAMP(10);
     if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
     return np_;
 }

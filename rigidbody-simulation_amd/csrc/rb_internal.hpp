@@ -217,7 +217,10 @@ template <typename T> struct HaloParams {
 };
 
 // launchers (rb_kernels.hip)
-template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, bool coop, hipStream_t s);
+// step kernel forms: one lane per body, 8 lanes per body (small scenes), one
+// lane per body at one wave per SIMD (mid-size scenes)
+enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2 };
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip

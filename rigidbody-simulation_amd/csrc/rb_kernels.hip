@@ -21,15 +21,7 @@
 //   thread of the same launch writes: Jacobi across bodies, exactly as
 //   multi_sphere_bounce.py:43-46 (one mj_forward per step).
 #include "rb_device.hpp"
-#include "rb_grid.hpp"
-#include "rb_internal.hpp"
 
-// diagnostic builds only (scripts/ablate.py): 1 = skip the sphere-sphere
-// broadphase, 2 = skip the world-inertia inverse (identity), 3 = empty
-// kernel (launch floor), 4 = search only (no body update), 0 = product
-#ifndef RB_ABLATE
-#define RB_ABLATE 0
-#endif
 // diagnostic build only: per-wave s_memtime stamps at phase boundaries
 #ifndef RB_STAMPS
 #define RB_STAMPS 0
@@ -46,6 +38,16 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][16];
     } while (0)
 #else
 #define STAMP(k) do {} while (0)
+#endif
+
+#include "rb_grid.hpp"
+#include "rb_internal.hpp"
+
+// diagnostic builds only (scripts/ablate.py): 1 = skip the sphere-sphere
+// broadphase, 2 = skip the world-inertia inverse (identity), 3 = empty
+// kernel (launch floor), 4 = search only (no body update), 0 = product
+#ifndef RB_ABLATE
+#define RB_ABLATE 0
 #endif
 
 namespace rb {
@@ -131,6 +133,16 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
     return search_buckets<T, MAXP>(p, i, x, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
         return candidate_hit(p, i, kind, x, rad, bi, tj, s);
     });
+}
+
+// K1, wide one-lane form (rb_grid.hpp search_buckets_wide)
+template <typename T, int MAXP, typename Overlap>
+__device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
+                                                        T rad, T bi, int32_t *s_id, uint32_t *s_cand, int tid,
+                                                        uint32_t gen, Overlap overlap) {
+    return search_buckets_wide<T, MAXP>(
+        p, i, x, s_id, s_cand, tid, gen,
+        [&](uint32_t tj, const Snap<T> &s) { return candidate_hit(p, i, kind, x, rad, bi, tj, s); }, overlap);
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
@@ -383,11 +395,13 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     STAMP(6);
 }
 
-// One body (G lanes): contact search, then (lane 0) the update.
-template <typename T, int MAXP, int G>
+// One body (G lanes): contact search, then (lane 0) the update.  WIDE: the
+// one-lane form for one wave per SIMD (search_buckets_wide; state loads and
+// inv(I_w) under the head loads).
+template <typename T, int MAXP, int G, bool WIDE>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
-                                          int32_t *cell, uint32_t gen) {
+                                          uint32_t *s_cand, int32_t *cell, uint32_t gen) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = p.lo + l;
@@ -404,14 +418,24 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     BodyIn<T> in;
     LazyInvI<T> invI;
     bool forced = false;
-    if constexpr (G > 1) {
+    constexpr bool early = G > 1 || WIDE;       // state loads issued before the search
+    if constexpr (early) {
         in = load_body(p, l, i);
         invI.I = in.I;
         invI.q = in.q;
     }
     STAMP(1);
     int32_t np_ = 0;
-    if constexpr (G == 1) {
+    if constexpr (G == 1 && WIDE) {
+        if (RB_ABLATE != 1)
+            np_ = search_partners_wide<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, s_cand, tid, gen, [&] {
+                invI.get();
+                if (!p.xfrc) {
+                    apply_force(p, l, in.m, invI, in.v, in.w);
+                    forced = true;
+                }
+            });
+    } else if constexpr (G == 1) {
         if (RB_ABLATE != 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid, gen);
     } else {
         if (RB_ABLATE != 1)
@@ -425,8 +449,9 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
                                           });
     }
     STAMP(2);
+    if (RB_ABLATE == 7) np_ = 0;                 // diagnostic: search, but solve no partner contact
     if (!active || k != 0 || RB_ABLATE == 4) return;
-    if constexpr (G == 1) {
+    if constexpr (!early) {
         in = load_body(p, l, i);
         invI.I = in.I;
         invI.q = in.q;
@@ -460,10 +485,11 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
     }
 }
 
-template <typename T, int MAXP, int G>
+template <typename T, int MAXP, int G, bool WIDE = false>
 __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
+    __shared__ uint32_t s_cand[WIDE ? WIDE_MAXC * NB : 1];
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
@@ -485,7 +511,8 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < p.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
-    if (G > 1 || active) body_step<T, MAXP, G>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, cell, gen);
+    if (G > 1 || active)
+        body_step<T, MAXP, G, WIDE>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen);
     if (p.bounds) fold_bounds(p.bounds, cell);
 }
 
@@ -510,6 +537,10 @@ __global__ __launch_bounds__(STEP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_G1)))
 #endif
 void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1>(p); }
+// one wave per SIMD (up to 64 x 1024 owned bodies): every register is free
+template <typename T, int MAXP>
+__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void step_kernel_wide(StepParams<T> p) { step_body<T, MAXP, 1, true>(p); }
 
 // ---- split form (large scenes): search kernel + update kernel -------------
 // The fused kernel's register footprint (the f64 solve) caps it at two
@@ -626,7 +657,8 @@ __global__ void kat_apply_kernel(int64_t n, const double *in, double *out) {
 }
 
 // ---- launchers ----------------------------------------------------------
-template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, bool coop, hipStream_t s) {
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, hipStream_t s) {
+    const bool coop = form == FORM_COOP;
     const int nb = coop ? STEP_BLOCK / 8 : STEP_BLOCK;
     int64_t blocks = (p.n_local + nb - 1) / nb;
     if (blocks < 1) blocks = 1;
@@ -643,6 +675,9 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, b
     } else if (coop) {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    } else if (form == FORM_WIDE) {
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     } else {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_one<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
@@ -675,8 +710,8 @@ template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, d
     return hipGetLastError();
 }
 
-template hipError_t launch_step<double>(const StepParams<double> &, int, bool, hipStream_t);
-template hipError_t launch_step<float>(const StepParams<float> &, int, bool, hipStream_t);
+template hipError_t launch_step<double>(const StepParams<double> &, int, int, hipStream_t);
+template hipError_t launch_step<float>(const StepParams<float> &, int, int, hipStream_t);
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
 template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
 template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *, hipStream_t);

@@ -31,6 +31,26 @@ import torch  # noqa: E402  (initialise torch's HIP context before the library's
 torch.cuda.init()
 from rbhip import _lib, scenes
 import rbhip.world as W
+
+
+def run_one(sc):
+    """Average step-kernel time (ms) of one world of scene sc."""
+    with W.World(sc) as w:
+        if os.environ.get("GRAPH", "1") == "1":
+            # K graph-replayed steps between HIP events on torch's stream
+            w.set_stream(torch.cuda.current_stream().cuda_stream)
+            w.step(60)
+            w.step(200)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(); w.step(200); e1.record(); torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / 200
+        w.step(60)
+        w.kernel_timing(True)
+        w.step(100)
+        return w.kernel_timing(False)[0]
+
+
 res = {}
 for rnd in range(2):
     for v in variants:
@@ -42,21 +62,11 @@ for rnd in range(2):
                 os.environ[name] = val
             for nx, ny in sizes:
                 sc = scenes.flat_spheres(nx, ny, seed=0)
-                with W.World(sc) as w:
-                    if os.environ.get("GRAPH", "1") == "1":
-                        # K graph-replayed steps between HIP events on torch's stream
-                        w.set_stream(torch.cuda.current_stream().cuda_stream)
-                        w.step(60)
-                        w.step(200)
-                        torch.cuda.synchronize()
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record(); w.step(200); e1.record(); torch.cuda.synchronize()
-                        avg = e0.elapsed_time(e1) / 200
-                    else:
-                        w.step(60)
-                        w.kernel_timing(True)
-                        w.step(100)
-                        avg, n = w.kernel_timing(False)
+                try:
+                    avg = run_one(sc)
+                except _lib.RbError as e:        # a diagnostic build may produce garbage
+                    print(f"{v} {env} N={nx * ny}: {e}", flush=True)
+                    continue
                 res.setdefault((v, env, nx * ny), []).append(avg)
             if env:
                 del os.environ[env.split("=")[0]]

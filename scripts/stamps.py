@@ -31,6 +31,11 @@ for nx, ny, warm in [(64, 64, 300), (256, 256, 60), (1024, 1024, 60)]:
     names = ["clear", "search", "load+grav", "solves", "pos+insert", "quat+store"]
     for k, nm in enumerate(names):
         print(f"   {nm:12s} median {int(np.median(d[:, k])):8d}  p90 {int(np.percentile(d[:, k], 90)):8d}")
+    if G == 1:  # one-lane search sub-phases
+        sub = [(1, 8, "snap+heads issue"), (8, 9, "heads+batch1"), (9, 10, "later batches"), (10, 2, "tail")]
+        for a, b_, nm in sub:
+            dd = buf[:, b_].astype(np.int64) - buf[:, a].astype(np.int64)
+            print(f"     {nm:16s} median {int(np.median(dd)):8d}  p90 {int(np.percentile(dd, 90)):8d}")
     if G > 1:   # cooperative search sub-phases
         sub = [(1, 8, "snap+cell"), (8, 9, "invI"), (9, 10, "bucket+test"), (10, 11, "place+sync"), (11, 2, "sort+sync")]
         for a, b_, nm in sub:
