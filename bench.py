@@ -136,6 +136,16 @@ class SingleWorldCheck:
         return bool(int(t.item()))
 
 
+def step_kernel_name(n_owned: int) -> str:
+    """The step kernel form the library picks for n_owned bodies
+    (rb_capi.hip launch_one: coop <= 32,768 < wide <= 65,536 < one)."""
+    if n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "32768")):
+        return "rb::step_kernel_coop"
+    if n_owned <= int(os.environ.get("RBHIP_WIDE_MAX_BODIES", "65536")):
+        return "rb::step_kernel_wide"
+    return "rb::step_kernel_one"
+
+
 def traffic_from_profiles(cfg: str, dtype: str):
     """HBM bytes per step-kernel launch from the committed PMC summary
     (profiles/pmc_traffic.json, written by profiles/collect_pmc.py)."""
@@ -251,8 +261,7 @@ def main():
                                     f"{args.warmup + 2 * args.steps} steps"} if P > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("rb::step_kernel_coop" if w.n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "32768"))
-                                else "rb::step_kernel_one"),
+                     "kernel": step_kernel_name(w.n_owned),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
