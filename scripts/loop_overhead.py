@@ -11,7 +11,7 @@ from rbhip import scenes
 from rbhip.shard import wrap_gpos
 
 K = 400
-sc = scenes.make("c2")
+sc = scenes.make(os.environ.get("CFG", "c2"))
 
 
 def timed(fn):
@@ -68,3 +68,12 @@ with rbhip.World(sc) as w:
     w.p2p_connect(w.p2p_handles())
     w.shard_run(K); torch.cuda.synchronize()
     print("shard_run (p2p, 1 rk)  host %.2f us/step  device %.2f us/step" % timed(lambda: w.shard_run(K)))
+
+# the peer-to-peer halo exchange with one rank: step kernel + push kernel +
+# insert kernel, no peers (the fixed cost a halo step adds)
+with rbhip.World(sc) as w:
+    w.set_stream(torch.cuda.current_stream().cuda_stream)
+    w.p2p_connect(w.p2p_handles())
+    w.p2p_halo(True)
+    w.shard_run(K); torch.cuda.synchronize()
+    print("shard_run (halo, 1 rk) host %.2f us/step  device %.2f us/step" % timed(lambda: w.shard_run(K)))
