@@ -638,12 +638,17 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxrec = 4 * w->n_planes + w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
-    // per-cell hash: 16 buckets per body (occupied cells <= bodies), so few
-    // cells share a bucket and few false candidates are read (measured: C3
-    // +15% over 4 per body); at most 2^26 buckets (8 GB of id lines)
-    int64_t hfac = 16;
-    if (const char *ev = getenv("RBHIP_HASH_FACTOR")) hfac = atoll(ev) > 0 ? atoll(ev) : 16;
-    int64_t want = hfac * w->N > 4096 ? hfac * w->N : 4096;
+    // per-cell hash, sized so few cells share a bucket and few false
+    // candidates are read: cooperative worlds (which also keep a slot
+    // snapshot line per bucket) 16 buckets per body; the one-lane and wide
+    // forms max(32 per body, 2^23) (measured against 16 per body: -8 % at
+    // 65,536 bodies, -2 % at 262k and 1M; 4 per body was 15 % slower than
+    // 16).  At most 2^26 buckets (8 GB of lines per table).
+    const bool coop_world = w->n_local <= w->coop_max;
+    int64_t want = coop_world ? 16 * w->N : (32 * w->N > (int64_t(1) << 23) ? 32 * w->N : (int64_t(1) << 23));
+    if (const char *ev = getenv("RBHIP_HASH_FACTOR"))
+        if (atoll(ev) > 0) want = atoll(ev) * w->N;
+    if (want < 4096) want = 4096;
     w->H = next_pow2(want < (int64_t(1) << 26) ? want : (int64_t(1) << 26));
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
