@@ -286,3 +286,23 @@ def test_kernel_timing_reports_launches(rb):
         avg, n = w.kernel_timing(False)
     assert n == 20 and 0 < avg < 50.0
     assert C.sizeof(C.c_double) == 8 and time.time() > 0
+
+
+def test_wide_form_on_contact_rich_scene_bit_exact(rb, oracle, monkeypatch):
+    """The wide one-lane form (32-byte bucket heads, LDS candidate list,
+    state loads under the search) on C2, 300 steps with many sphere-sphere
+    contacts and buckets of several bodies: contacts and state bit-exact
+    with the oracle."""
+    from rbhip import scenes
+    monkeypatch.setenv("RBHIP_COOP_MAX_BODIES", "0")        # 4,096 bodies through the wide form
+    sc = scenes.make("c2")
+    q0, v0, (cnt, par, kin, dis) = _oracle_run(oracle, sc, 300, record=True)
+    with rb.World(sc) as w:
+        w.step(299)
+        w.record_contacts(True)
+        w.step(1)
+        q, v = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert np.array_equal(q, q0) and np.array_equal(v, v0)
+    assert (kin == 16).sum() > 100
