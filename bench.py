@@ -18,8 +18,9 @@ pushes for shards this large).
 N > 1 is validated: after the warmup and again after the timed region, every
 rank's bodies must be bit-identical to one World of the whole scene stepped
 the same number of steps on rank 0's GPU.  A transport that fails the first
-check (or times out) is replaced by the next (p2p -> rccl); one that fails
-the second makes the run exit non-zero instead of printing a number.
+check (or times out) is replaced by the next (p2p halo -> p2p full reads
+-> rccl); one that fails the second makes the run exit non-zero instead of
+printing a number.
 
 value = total bodies x K / (max over ranks of the timed region), with the
 state resident in HBM.  roofline: algorithmic HBM bytes of the step kernel
@@ -181,9 +182,11 @@ def main():
 
     scene, desc = make_scene(args.config, P)
     check = SingleWorldCheck(scene, args.dtype, device, rank, P) if P > 1 else None
-    transports = [None, "rccl"] if P > 1 else [None]
-    for k, tr in enumerate(transports):
-        sw = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr)
+    # (transport, halo): the library's default (peer-to-peer, halo for large
+    # shards), then peer-to-peer full reads, then RCCL
+    transports = [(None, "auto"), ("p2p", False), ("rccl", "auto")] if P > 1 else [(None, "auto")]
+    for k, (tr, halo) in enumerate(transports):
+        sw = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo)
         # warmup (also builds and caches the K-step graphs)
         sw.step(args.warmup)
         if check is None or check(sw, args.warmup):
@@ -193,8 +196,8 @@ def main():
         if k + 1 == len(transports):
             raise SystemExit(f"bench: every transport failed validation (last: {name})")
         if rank == 0:
-            print(f"bench: {name} exchange failed validation; falling back to {transports[k + 1]}",
-                  file=sys.stderr, flush=True)
+            print(f"bench: {name} exchange failed validation; falling back to {transports[k + 1][0]}"
+                  f"{'' if transports[k + 1][1] else ' (full reads)'}", file=sys.stderr, flush=True)
     w = sw.world
     sw.sync()
 
