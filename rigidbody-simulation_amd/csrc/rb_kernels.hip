@@ -501,11 +501,17 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     asm volatile("" ::"s"(p.snap_cur), "s"(p.st.base), "s"(p.st.S), "s"(p.cs.base), "s"(p.cs.Npad), "s"(p.cs.kind),
                  "s"(p.n_local), "s"(p.lo));
 
-    if (p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;   // peer-to-peer exchange: this step's number
-    // generation of the table this step reads; the next table's is one more
-    // (published by block 0 for the kernels that insert after this one)
+    // Block 0 advances the exchange's step number and publishes the next
+    // table's generation (one more than the one this step reads) for the
+    // kernels that insert after this one.  The cooperative form does it at
+    // the end: a store ahead of the body loads holds them back (they may not
+    // pass it), which cost its waves a scalar round trip (+11 % at 16k
+    // bodies).  The one-lane forms measured no gain (65k) or a loss (1M).
+    constexpr bool late_publish = G > 1;
+    if constexpr (late_publish) asm volatile("" ::"s"(p.cur.gen));   // with the prologue's scalar loads
+    if (!late_publish && p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;
     const uint32_t gen = *p.cur.gen;
-    if (p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
+    if (!late_publish && p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
 
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
@@ -514,6 +520,10 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     if (G > 1 || active)
         body_step<T, MAXP, G, WIDE>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen);
     if (p.bounds) fold_bounds(p.bounds, cell);
+    if (late_publish && blockIdx.x == 0 && tid == 0) {
+        if (p.next.line) *p.next.gen = gen + 1u;
+        if (p.epoch) *p.epoch += 1;
+    }
 }
 
 // The two forms as separate kernels: the one-lane (large-scene) form may be
