@@ -668,9 +668,10 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
     ALLOC(w->gen, sizeof(uint32_t) * 2);
-    // Experimental, opt-in (RBHIP_SPLIT=1): large scenes step in two kernels
-    // (search, update) joined by a partner list.  Not yet validated on the
-    // device; the default is the fused one-kernel step.
+    // Opt-in (RBHIP_SPLIT=1): large scenes step in two kernels (search,
+    // update) joined by a partner list; bit-exact with the oracle on the
+    // device (tests/test_gpu_parity.py ragged-scene test) but no faster
+    // (DESIGN §5), so the default is the fused one-kernel step.
     const char *split_env = getenv("RBHIP_SPLIT");
     const bool coop = w->n_local <= w->coop_max;
     const bool split = !coop && split_env && atoi(split_env) == 1;

@@ -306,3 +306,33 @@ def test_wide_form_on_contact_rich_scene_bit_exact(rb, oracle, monkeypatch):
     assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
     assert np.array_equal(q, q0) and np.array_equal(v, v0)
     assert (kin == 16).sum() > 100
+
+
+@pytest.mark.parametrize("form,env", [
+    ("coop", {}),
+    ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+    ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"}),
+    ("split", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0", "RBHIP_SPLIT": "1"}),
+])
+def test_ragged_scene_every_step_form_bit_exact(rb, oracle, monkeypatch, form, env):
+    """A body count that fills no workgroup evenly (37 x 29 = 1,073; the last
+    wave is partial) on a packed grid (spacing 0.19 < 2r: neighbours collide
+    once they land), through each step form the library can pick: 120
+    steps, then one recorded step, contacts and state bit-exact with the
+    oracle."""
+    from rbhip import scenes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = scenes.flat_spheres(37, 29, seed=3, spacing=0.19)
+    assert sc.n % 64 != 0
+    q0, v0, (cnt, par, kin, dis) = _oracle_run(oracle, sc, 121, record=True)
+    with rb.World(sc) as w:
+        w.step(120)
+        w.record_contacts(True)
+        w.step(1)
+        q, v = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert np.array_equal(gd, dis)
+    assert np.array_equal(q, q0) and np.array_equal(v, v0)
+    assert (kin == 16).sum() > 50                      # sphere-sphere contacts in the recorded step
