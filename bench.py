@@ -139,8 +139,8 @@ class SingleWorldCheck:
 
 def step_kernel_name(n_owned: int) -> str:
     """The step kernel form the library picks for n_owned bodies
-    (rb_capi.hip launch_one: coop <= 32,768 < wide <= 65,536 < one)."""
-    if n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "32768")):
+    (rb_capi.hip launch_one: coop <= 20,480 < wide <= 65,536 < one)."""
+    if n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "20480")):
         return "rb::step_kernel_coop"
     if n_owned <= int(os.environ.get("RBHIP_WIDE_MAX_BODIES", "65536")):
         return "rb::step_kernel_wide"

@@ -1,6 +1,6 @@
 """Diagnostic: time the step kernel (graph replay, or GRAPH=0: HIP events per launch) for several
 builds (VARIANTS: ";"-separated extra compiler flags) and runtime settings
-(ENVS: ";"-separated NAME=VALUE applied before each world is created), over
+(ENVS: ";"-separated entries of ","-separated NAME=VALUE applied before each world is created), over
 several flat-sphere scene sizes, interleaved in one process.  Not part of the
 product; results go to stdout."""
 import os, subprocess, sys
@@ -57,8 +57,9 @@ for rnd in range(2):
         _lib._lib = None
         _lib.load(paths[v])
         for env in envs:
-            if env:
-                name, val = env.split("=")
+            # an ENVS entry may set several variables: NAME=VALUE,NAME=VALUE
+            assigns = [a.split("=") for a in env.split(",")] if env else []
+            for name, val in assigns:
                 os.environ[name] = val
             for nx, ny in sizes:
                 sc = scenes.flat_spheres(nx, ny, seed=0)
@@ -68,7 +69,7 @@ for rnd in range(2):
                     print(f"{v} {env} N={nx * ny}: {e}", flush=True)
                     continue
                 res.setdefault((v, env, nx * ny), []).append(avg)
-            if env:
-                del os.environ[env.split("=")[0]]
+            for name, _ in assigns:
+                del os.environ[name]
 for (v, env, n), t in sorted(res.items(), key=lambda kv: (kv[0][2], kv[0][0], kv[0][1])):
     print(f"N={n:8d} {v:20s} {env:34s} kernel ms {min(t):.4f} -> {n / min(t) / 1e6:7.2f} G body-steps/s")

@@ -15,9 +15,9 @@ import rbhip.world as W
 L = _lib.load("/tmp/libstamp.so")
 L.rb_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 for nx, ny, warm in [(64, 64, 300), (256, 256, 60), (1024, 1024, 60)]:
-    if nx * ny * (8 if nx * ny <= 32768 else 1) > 64 * (1 << 16): continue
+    if nx * ny * (8 if nx * ny <= 20480 else 1) > 64 * (1 << 16): continue
     sc = scenes.flat_spheres(nx, ny, seed=0)
-    G = 8 if sc.n <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "32768")) else 1
+    G = 8 if sc.n <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "20480")) else 1
     nb = (sc.n * G + 63) // 64
     with W.World(sc) as w:
         w.step(warm)
