@@ -1,44 +1,62 @@
 """Benchmark: body-steps/s of the rigid-body hot path on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--dtype f64]
+                    [--scaling strong|weak]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
 Workload: C3 (BASELINE.json configs[2]) in fp64 — 65,536 spheres r 0.1 on
 flat ground, e 0.8, mu 0.3, dt 0.01, seeded synthetic initial conditions
 (rbhip.scenes.flat_spheres).  That is the scene the north-star
 target is quoted on ("≥1M body-steps/sec on a 65 536-sphere scene at
-1×MI355X with ≥3.5× at 8 GPUs"); `--config c2` runs configs[1] (4,096
-spheres), c4 / c5 the incline and cube scenes.  A "step" is one reference
-step of the whole scene (contacts, impulses, integration).  With N ranks
-the scene is N such 256x256 patches side by side on one shared ground (weak
-scaling: 65,536 bodies per GPU); rank r owns patch r, and the ranks exchange
-positions inside the library every step (peer-to-peer over xGMI: halo
-pushes for shards this large).
+1×MI355X with ≥3.5× at 8 GPUs").  `--config c4` is configs[3] (65,536
+spheres on the 0.7 rad incline, friction-dominated, "sharded 8×MI355X"),
+c2 configs[1] (4,096 spheres), c5 configs[4] (16,384 cubes).  A "step" is
+one reference step of the whole scene (contacts, impulses, integration:
+the body loop of multi_sphere_bounce.py:42-92).
+
+Scaling (body-id range shards, positions exchanged every step):
+  strong (default)  the SAME scene split over the N ranks: rank r owns body
+                    ids [r*S, r*S+S), S = ceil(N_bodies / N) — for C3 a slab
+                    of 256/N grid rows.  This is the north-star's "≥3.5× at
+                    8 GPUs" on one 65,536-sphere scene; N = 1 is the BENCH line.
+  weak              N patches of the config side by side on one shared
+                    ground, one per rank (per-GPU work fixed).
+The ranks exchange positions inside the library every step (peer-to-peer
+over xGMI; halo pushes for slabs of >= rbhip.shard.HALO_MIN_SHARD bodies).
 
 N > 1 is validated: after the warmup and again after the timed region, every
-rank's bodies must be bit-identical to one World of the whole scene stepped
-the same number of steps on rank 0's GPU.  A transport that fails the first
-check (or times out) is replaced by the next (p2p halo -> p2p full reads
--> rccl); one that fails the second makes the run exit non-zero instead of
-printing a number.
+rank's bodies must be bit-identical (compared as uint64 words, so the sign
+of zeros counts) to one World of the whole scene stepped the same number of
+steps on rank 0's GPU.  A transport that fails the first check (or times
+out) is replaced by the next (p2p default -> p2p full reads -> rccl); one
+that fails the second makes the run exit non-zero instead of printing a
+number.
 
 value = total bodies x K / (max over ranks of the timed region), with the
-state resident in HBM.  roofline: algorithmic HBM bytes of the step kernel
-(248 B per sphere body-step in fp64) x owned bodies / its
-average launch duration.  One rank: HIP events recorded on the world's
-stream (torch's current stream) around the timed region, which is exactly K
-graph-replayed step-kernel launches, / K.  Several ranks: an event pair
-around each step-kernel launch over a second run of K steps.
-cpu_baseline: the oracle (C restatement of the reference arithmetic) on rank 0
-at N=1 over the full single-GPU scene for --cpu-steps steps from t = 0, on
-the GPU's host-core share (OMP_NUM_THREADS, 16 on the GPU box) and on one
-core.
+state resident in HBM.  The timed steps are steps W+K+1 .. W+2K from t = 0
+(the K steps before them capture the K-step graph): `timed_steps`.
+roofline: algorithmic HBM bytes of the step kernel (248 B per
+sphere body-step in fp64) x owned bodies / its average launch duration.
+One rank: HIP events recorded on the world's stream (torch's current
+stream) around the timed region, which is exactly K graph-replayed
+step-kernel launches, / K.  Several ranks: an event pair around each
+step-kernel launch over a second run of K steps.  `traffic` /
+`traffic_lower`: the PMC bounds per launch from the committed
+profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
+command, profiles/collect_pmc.py), named in `traffic_source`.
+cpu_baseline (rank 0, N = 1): the oracle (C restatement of the reference
+arithmetic) over the full single-GPU scene for --cpu-steps steps from t = 0,
+on the host-core share (OMP_NUM_THREADS if set, else the affinity mask) and
+on one core, with the host's nproc / affinity / CPU model.  `accuracy`: the
+GPU state after the same --cpu-steps steps against that oracle run (BASELINE
+metric "CPU-ref max|Δpos|"), and whether the last step's contact lists agree.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -46,6 +64,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rigidbody-simulation_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+CONFIG_DESC = {
+    "c2": "c2 (BASELINE configs[1]): 4096 spheres, flat ground",
+    "c3": "c3 (BASELINE configs[2]): 65536 spheres, flat ground",
+    "c4": "c4 (BASELINE configs[3]): 65536 spheres, 0.7 rad incline (friction-dominated)",
+    "c5": "c5 (BASELINE configs[4]): 16384 cubes, 0.7 rad incline",
+}
+TILE = {"c2": (64, 64), "c3": (256, 256), "c4": (256, 256), "c5": (128, 128)}
 
 
 def parse():
@@ -55,43 +80,106 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=200)
     return ap.parse_args()
 
 
-def make_scene(cfg: str, P: int):
+def make_scene(cfg: str, P: int, scaling: str):
+    """The scene all ranks step together, and its description."""
     from rbhip import scenes
-    if cfg == "c2":
-        return scenes.tiled(scenes.flat_spheres, P, 64, 64, seed=0), "c2: 4096 spheres/GPU, flat ground"
-    if cfg == "c3":
-        return scenes.tiled(scenes.flat_spheres, P, 256, 256, seed=0), "c3: 65536 spheres/GPU, flat ground"
-    if cfg == "c4":
-        return scenes.tiled(scenes.incline_spheres, P, 256, 256, seed=0), "c4: 65536 spheres/GPU, 0.7 rad incline"
-    return scenes.tiled(scenes.incline_cubes, P, 128, 128, seed=0), "c5: 16384 cubes/GPU, 0.7 rad incline"
+    if scaling == "strong" or P == 1:
+        desc = CONFIG_DESC[cfg] + (f", one scene sharded over {P} GPUs (strong scaling)" if P > 1 else "")
+        return scenes.make(cfg), desc
+    fn = {"c2": scenes.flat_spheres, "c3": scenes.flat_spheres, "c4": scenes.incline_spheres,
+          "c5": scenes.incline_cubes}[cfg]
+    nx, ny = TILE[cfg]
+    return scenes.tiled(fn, P, nx, ny, seed=0), CONFIG_DESC[cfg] + f" per GPU, {P} patches (weak scaling)"
+
+
+def host_facts() -> dict:
+    """The CPU the baseline ran on: nproc, affinity mask size, model name (lscpu)."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.lower().startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    if model is None:
+        try:
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("model name"):
+                        model = line.split(":", 1)[1].strip()
+                        break
+        except OSError:
+            pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model}
 
 
 def cpu_baseline(cfg: str, steps: int):
     """Oracle (C restatement of the reference arithmetic) on the single-GPU
-    scene, on all of this GPU's host-core share (OpenMP over bodies) and on
-    one core; returns the cpu_baseline dict."""
+    scene, on this GPU's host-core share (OpenMP over bodies) and on one
+    core.  Returns (cpu_baseline dict, the multi-core run's final state and
+    last-step contacts) — the latter is the accuracy reference."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    sc, _ = make_scene(cfg, 1)
+    sc, _ = make_scene(cfg, 1, "strong")
     osc = O.OracleScene(sc)
-    cores = int(os.environ.get("OMP_NUM_THREADS", "16"))
-    rates = {}
-    for th in (cores, 1):
+    host = host_facts()
+    cores = int(host["omp_num_threads"]) if host["omp_num_threads"] else host["affinity"]
+    rates, ref = {}, None
+    for th in dict.fromkeys((cores, 1)):
         O.set_threads(th)
         t0 = time.perf_counter()
-        O.step(osc, sc.qpos0, sc.qvel0, steps)
-        rates[th] = (sc.n * steps / (time.perf_counter() - t0), time.perf_counter() - t0)
-    return {"value": rates[cores][0], "unit": "body-steps/s", "cores": cores, "kind": "port",
-            "value_1core": rates[1][0],
+        res = O.step(osc, sc.qpos0, sc.qvel0, steps, record=(th == cores))
+        el = time.perf_counter() - t0
+        rates[th] = (sc.n * steps / el, el)
+        if th == cores:
+            ref = res
+    base = {"value": rates[cores][0], "unit": "body-steps/s", "cores": cores, "kind": "port",
+            "value_1core": rates[1][0], "host": host,
             "sample": f"oracle/rb_oracle.c (C restatement of collision.py/physics_utils.py/"
                       f"multi_sphere_bounce.py arithmetic, bit-identical to the GPU path) on the full {cfg} "
                       f"scene, {sc.n} bodies x {steps} steps from t=0: {cores} OpenMP threads "
                       f"{rates[cores][1]:.1f} s, 1 thread {rates[1][1]:.1f} s"}
+    return base, ref
+
+
+def accuracy(cfg: str, dtype: str, device: int, steps: int, ref) -> dict:
+    """GPU state after `steps` steps from t = 0 vs the fp64 oracle run
+    (BASELINE metric "CPU-ref max|Δpos|"; the state written at
+    multi_sphere_bounce.py:85-88) and the last step's contact lists."""
+    import numpy as np
+    import rbhip
+    sc, _ = make_scene(cfg, 1, "strong")
+    q_ref, v_ref, (cnt, par, kin, dis) = ref
+    with rbhip.World(sc, device=device, dtype=dtype) as w:
+        if steps > 1:
+            w.step(steps - 1)
+        w.record_contacts(True)
+        w.step(1)
+        q, v = w.get_state()
+        gc, gp, gk, _ = w.contacts()
+    dx = np.linalg.norm(q[:, :3] - q_ref[:, :3], axis=1)
+    dv = np.linalg.norm(v - v_ref, axis=1)
+    rel_x = dx / np.maximum(np.linalg.norm(q_ref[:, :3], axis=1), 1e-12)
+    rel_v = dv / np.maximum(np.linalg.norm(v_ref, axis=1), 1e-12)
+    return {"vs": "oracle fp64 (cpu_baseline run), same initial conditions",
+            "steps": steps, "dtype": dtype,
+            "max_abs_dpos": float(np.abs(q[:, :3] - q_ref[:, :3]).max()),
+            "max_rel_dpos": float(rel_x.max()), "max_rel_dvel": float(rel_v.max()),
+            "median_rel_dpos": float(np.median(rel_x)),
+            "contacts_equal": bool(np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)),
+            "contacts_last_step": int(cnt.sum()),
+            "bit_identical": bool(np.array_equal(q.view(np.uint64), q_ref.view(np.uint64)) and
+                                  np.array_equal(v.view(np.uint64), v_ref.view(np.uint64))),
+            "definition": "rel = |d| / |ref| per body (position 3-vector; velocity 6-vector incl. spin)"}
 
 
 class SingleWorldCheck:
@@ -127,9 +215,12 @@ class SingleWorldCheck:
             self.ref.step(steps_total - self.done)
             self.done = steps_total
             q1, v1 = self.ref.get_state()
-            same = int(np.array_equal(q, q1) and np.array_equal(v, v1))
+            # as 64-bit words: -0.0 and +0.0 differ
+            same = int(np.array_equal(q.view(np.uint64), q1.view(np.uint64)) and
+                       np.array_equal(v.view(np.uint64), v1.view(np.uint64)))
             if not same:
-                bad = np.flatnonzero(~(np.all(q == q1, axis=1) & np.all(v == v1, axis=1)))
+                bad = np.flatnonzero(~(np.all(q.view(np.uint64) == q1.view(np.uint64), axis=1) &
+                                       np.all(v.view(np.uint64) == v1.view(np.uint64), axis=1)))
                 print(f"bench: {bad.size} bodies differ from the single World after {steps_total} steps "
                       f"(first ids {bad[:8].tolist()})", file=sys.stderr, flush=True)
         t = torch.tensor([same], device=dev)
@@ -147,15 +238,21 @@ def step_kernel_name(n_owned: int) -> str:
     return "rb::step_kernel_one"
 
 
-def traffic_from_profiles(cfg: str, dtype: str):
-    """HBM bytes per step-kernel launch from the committed PMC summary
-    (profiles/pmc_traffic.json, written by profiles/collect_pmc.py)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str):
+    """(upper, lower, source) HBM bytes per step-kernel launch from the
+    committed PMC summary (profiles/pmc_traffic.json, profiles/collect_pmc.py);
+    keyed by config and dtype for one GPU, with a _p<N> suffix for strong
+    shards.  (None, None, None) when that shape was never collected."""
+    rel = os.path.join("profiles", "pmc_traffic.json")
+    key = f"{cfg}_{dtype}" if P == 1 or scaling == "weak" else f"{cfg}_{dtype}_p{P}"
     try:
-        with open(p) as f:
-            return json.load(f).get(f"{cfg}_{dtype}", {}).get("hbm_bytes_per_launch")
+        with open(os.path.join(ROOT, rel)) as f:
+            e = json.load(f).get(key)
     except (OSError, ValueError):
-        return None
+        e = None
+    if not e:
+        return None, None, None
+    return e.get("hbm_bytes_per_launch"), e.get("hbm_bytes_per_launch_lower"), f"{rel}[{key}]"
 
 
 def main():
@@ -180,7 +277,7 @@ def main():
             dist.init_process_group(backend)
     from rbhip.shard import ShardedWorld
 
-    scene, desc = make_scene(args.config, P)
+    scene, desc = make_scene(args.config, P, args.scaling)
     check = SingleWorldCheck(scene, args.dtype, device, rank, P) if P > 1 else None
     # (transport, halo): the library's default (peer-to-peer, halo for large
     # shards), then peer-to-peer full reads, then RCCL
@@ -219,6 +316,7 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
+    timed = [args.warmup + args.steps + 1, args.warmup + 2 * args.steps]
     if P > 1:
         t = torch.tensor([elapsed], device=f"cuda:{device}" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -240,7 +338,7 @@ def main():
         timing = "HIP event pair around each step-kernel launch (second run of K steps)"
     bytes_per_launch = w.bytes_per_body_step * w.n_owned
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = traffic_from_profiles(args.config, args.dtype)
+    traffic, traffic_lower, traffic_src = traffic_from_profiles(args.config, args.dtype, P, args.scaling)
 
     value = scene.n * args.steps / elapsed
     line = {
@@ -252,25 +350,31 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded rbhip.scenes, SURVEY 8d)",
+        "timed_steps": timed,
         "config": {"workload": desc, "bodies_total": scene.n, "bodies_per_gpu": w.n_owned,
                    "parallelism": f"body-range shards x{P}" + (
                        f", {sw.transport}{' halo' if sw.halo else ''} position exchange, graph-replayed" if P > 1 else ""),
+                   "timed_steps": timed,
                    "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction,
-                   **({"validated": f"bit-identical to one World of the whole scene after {args.warmup} and "
-                                    f"{args.warmup + 2 * args.steps} steps"} if P > 1 else {})},
+                   **({"validated": f"bit-identical (uint64 words) to one World of the whole scene after "
+                                    f"{args.warmup} and {args.warmup + 2 * args.steps} steps"} if P > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": traffic_lower,
+                     "traffic_source": traffic_src,
                      "kernel": step_kernel_name(w.n_owned),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
     if rank == 0 and P == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_steps)
+        w.close()
+        base, ref = cpu_baseline(args.config, args.cpu_steps)
+        line["cpu_baseline"] = base
+        line["accuracy"] = accuracy(args.config, args.dtype, device, args.cpu_steps, ref)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if P > 1:

@@ -126,7 +126,12 @@ struct rb_world {
     // and bucket slots mod 2
     int64_t c = 0;
     bool primed = false;
-    std::map<std::tuple<int64_t, int, double, double, double, double, int>, hipGraphExec_t> graphs;
+    // captured K-step graphs, least recently used evicted past GRAPH_CACHE_MAX
+    // entries (a caller stepping varying chunk lengths would otherwise keep
+    // accumulating executables)
+    struct GraphEntry { hipGraphExec_t ex; uint64_t used; };
+    std::map<std::tuple<int64_t, int, double, double, double, double, int>, GraphEntry> graphs;
+    uint64_t graph_tick = 0;
     // kernel timing
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
@@ -403,8 +408,21 @@ int shard_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, double
 }
 
 void drop_graphs(rb_world *w) {
-    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second.ex);
     w->graphs.clear();
+}
+
+constexpr size_t GRAPH_CACHE_MAX = 32;
+
+// evict least recently used graphs until `room` more fit
+void evict_graphs(rb_world *w, size_t room) {
+    while (!w->graphs.empty() && w->graphs.size() + room > GRAPH_CACHE_MAX) {
+        auto lru = w->graphs.begin();
+        for (auto it = w->graphs.begin(); it != w->graphs.end(); ++it)
+            if (it->second.used < lru->second.used) lru = it;
+        (void)hipGraphExecDestroy(lru->second.ex);
+        w->graphs.erase(lru);
+    }
 }
 
 // Table generations are 32-bit and only grow: before they would wrap (after
@@ -414,7 +432,9 @@ void drop_graphs(rb_world *w) {
 int gen_guard(rb_world *w, int64_t nsteps) {
     const uint64_t g = (uint32_t)(w->gen_off + (uint32_t)w->c);
     if (g + (uint64_t)nsteps + 4 < (1ull << 32)) return RB_OK;
-    if (w->halo) return fail(RB_EOVERFLOW, "table generations exhausted: call rb_set_state to restart the halo exchange");
+    if (w->halo)
+        return fail(RB_EOVERFLOW, "table generations exhausted after ~4e9 steps of a halo-exchanging shard: "
+                                  "the sharded world must be recreated");
     HIPCHK(hipStreamSynchronize(w->stream));
     for (int k = 0; k < 2; ++k) HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
     w->gen_off = 1u - (uint32_t)w->c;   // prime() makes step c's generation 2
@@ -465,7 +485,7 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
         auto it = w->graphs.find(key);
         if (it == w->graphs.end()) {
-            if (w->graphs.size() >= 60) drop_graphs(w);
+            evict_graphs(w, 2);
             // capture both parities at once, so later calls starting at
             // either replay without a capture
             for (int c0 = 0; c0 < 2; ++c0) {
@@ -479,11 +499,12 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
                 HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
                 HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
                 (void)hipGraphDestroy(graph);
-                w->graphs[std::make_tuple(K, c0, dt, e, mu, thr, variant)] = ex;
+                w->graphs[std::make_tuple(K, c0, dt, e, mu, thr, variant)] = rb_world::GraphEntry{ex, 0};
             }
             it = w->graphs.find(key);
         }
-        HIPCHK(hipGraphLaunch(it->second, w->stream));
+        it->second.used = ++w->graph_tick;
+        HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
         w->c += K;
         left -= K;
     }
@@ -652,7 +673,16 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_HASH_FACTOR"))
         if (atoll(ev) > 0) want = atoll(ev) * w->N;
     if (want < 4096) want = 4096;
-    w->H = next_pow2(want < (int64_t(1) << 26) ? want : (int64_t(1) << 26));
+    // memory cap over both tables (lines, plus slot snapshots in cooperative
+    // worlds): RBHIP_HASH_MAX_BYTES, default 8 GiB (1M bodies keep 32 buckets
+    // per body, 4M bodies get 8)
+    const int64_t per_bucket = 2 * (int64_t)(sizeof(uint32_t) * LINE_WORDS + (coop_world ? w->esz * 4 * LINE_WORDS : 0));
+    int64_t cap_bytes = int64_t(8) << 30;
+    if (const char *ev = getenv("RBHIP_HASH_MAX_BYTES"))
+        if (atoll(ev) > 0) cap_bytes = atoll(ev);
+    int64_t hmax = 4096;
+    while (hmax * 2 * per_bucket <= cap_bytes && hmax < (int64_t(1) << 26)) hmax *= 2;
+    w->H = next_pow2(want) < hmax ? next_pow2(want) : hmax;
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
     // algorithmic bytes per body-step: 13 state reals read + 13
@@ -943,10 +973,7 @@ int rb_record_contacts(rb_world *w, int enable) {
         HIPCHK(hipMalloc(&w->rec_dist, (size_t)w->esz * slots));
         HIPCHK(hipMemset(w->rec_count, 0, sizeof(int32_t) * w->S));
     }
-    if (w->record != (enable != 0)) {
-        for (auto &kv : w->graphs) (void)hipGraphExecDestroy(kv.second);
-        w->graphs.clear();
-    }
+    if (w->record != (enable != 0)) drop_graphs(w);
     w->record = enable != 0;
     return RB_OK;
 }
@@ -1033,6 +1060,9 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
     if (!w) return fail(RB_EINVAL, "null world");
     if (law != RB_LAW_MUJOCO && law != RB_LAW_BALLS) return fail(RB_EINVAL, "unknown contact law %d", law);
     if (!(tol >= 0) || !(tol < 1e6)) return fail(RB_EINVAL, "tol must be finite and >= 0");
+    // a law change rebuilds the table from the local snapshot, whose rows of
+    // bodies no peer pushed to this rank are stale in halo mode
+    if (w->halo) return fail(RB_EUNSUPPORTED, "rb_set_contact_law on a halo-exchanging shard");
     if (law == RB_LAW_BALLS) {
         if (!w->all_spheres) return fail(RB_EUNSUPPORTED, "the two-ball law takes spheres only");
         if (w->P != 1) return fail(RB_EUNSUPPORTED, "the two-ball law steps unsharded worlds only");

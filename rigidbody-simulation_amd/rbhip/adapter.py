@@ -70,34 +70,66 @@ class SceneData:
         self.ncon = 0
 
 
-def scene_from_mujoco(model) -> Scene:
+def _mujoco():
+    import mujoco
+    return mujoco
+
+
+def free_bodies(model) -> list:
+    """Body ids of the free bodies, in body order.  SceneModel: bodies
+    FIRST..nbody-1; a MuJoCo model: every body whose single joint is a free
+    joint (body_jntnum / body_jntadr / jnt_type)."""
+    if isinstance(model, SceneModel):
+        return list(range(SceneModel.FIRST, model.nbody))
+    mj = _mujoco()
+    return [b for b in range(model.nbody) if model.body_jntnum[b] == 1 and
+            model.jnt_type[model.body_jntadr[b]] == mj.mjtJoint.mjJNT_FREE]
+
+
+def state_index(model):
+    """(qpos index [nfree, 7], qvel index [nfree, 6]) of the free bodies'
+    joints: jnt_qposadr / jnt_dofadr for a MuJoCo model (joints need not be
+    contiguous or start at 0), stride 7 / 6 for a SceneModel."""
+    fb = free_bodies(model)
+    if isinstance(model, SceneModel):
+        k = np.arange(len(fb))
+        return 7 * k[:, None] + np.arange(7), 6 * k[:, None] + np.arange(6)
+    qa = np.array([model.jnt_qposadr[model.body_jntadr[b]] for b in fb], dtype=np.int64)
+    da = np.array([model.jnt_dofadr[model.body_jntadr[b]] for b in fb], dtype=np.int64)
+    return qa[:, None] + np.arange(7), da[:, None] + np.arange(6)
+
+
+def scene_from_mujoco(model, restitution: float = 1.0, friction: float = 0.5) -> Scene:
     """Scene from a compiled mujoco.MjModel (free bodies with one sphere or
-    box geom each; planes on static bodies).  Parity of this path is
-    unpinned: MuJoCo is not installed in the build container."""
-    import mujoco  # noqa: F401
-    d = mujoco.MjData(model)
-    mujoco.mj_forward(model, d)
-    free = [b for b in range(model.nbody) if model.body_jntnum[b] == 1 and
-            model.jnt_type[model.body_jntadr[b]] == mujoco.mjtJoint.mjJNT_FREE]
+    box geom each; planes on static bodies).  restitution / friction are the
+    scene's defaults only — every step call passes the caller's values
+    (collision.py:56-61).  Parity of this path is unpinned: MuJoCo is not
+    installed in the build container (tested with a duck-typed fake)."""
+    mj = _mujoco()
+    d = mj.MjData(model)
+    mj.mj_forward(model, d)
+    free = free_bodies(model)
     kind, size = [], []
     planes = []
     for g in range(model.ngeom):
         t = model.geom_type[g]
-        if t == mujoco.mjtGeom.mjGEOM_PLANE:
-            mat = d.geom_xmat[g].reshape(3, 3)
+        if t == mj.mjtGeom.mjGEOM_PLANE:
+            mat = np.asarray(d.geom_xmat[g]).reshape(3, 3)
             planes.append(np.concatenate([mat[:, 2], d.geom_xpos[g]]))
     for b in free:
         gs = [g for g in range(model.ngeom) if model.geom_bodyid[g] == b]
-        if len(gs) != 1 or model.geom_type[gs[0]] not in (mujoco.mjtGeom.mjGEOM_SPHERE, mujoco.mjtGeom.mjGEOM_BOX):
+        if len(gs) != 1 or model.geom_type[gs[0]] not in (mj.mjtGeom.mjGEOM_SPHERE, mj.mjtGeom.mjGEOM_BOX):
             raise NotImplementedError("each free body must carry exactly one sphere or box geom")
         g = gs[0]
-        kind.append(SPHERE if model.geom_type[g] == mujoco.mjtGeom.mjGEOM_SPHERE else BOX)
-        size.append(model.geom_size[g].copy())
-    qpos = np.stack([d.qpos[model.jnt_qposadr[model.body_jntadr[b]]:][:7] for b in free])
-    qvel = np.stack([d.qvel[model.jnt_dofadr[model.body_jntadr[b]]:][:6] for b in free])
-    return Scene("mujoco", np.array(kind, np.int32), model.body_mass[free].copy(),
-                 model.body_inertia[free].copy(), np.array(size), np.array(planes).reshape(-1, 6),
-                 qpos, qvel, dt=float(model.opt.timestep), restitution=1.0, friction=0.5,
+        kind.append(SPHERE if model.geom_type[g] == mj.mjtGeom.mjGEOM_SPHERE else BOX)
+        size.append(np.asarray(model.geom_size[g], dtype=np.float64).copy())
+    qi, vi = state_index(model)
+    qpos = np.asarray(d.qpos, dtype=np.float64)[qi]
+    qvel = np.asarray(d.qvel, dtype=np.float64)[vi]
+    return Scene("mujoco", np.array(kind, np.int32), np.asarray(model.body_mass, np.float64)[free].copy(),
+                 np.asarray(model.body_inertia, np.float64)[free].copy(), np.array(size),
+                 np.array(planes, dtype=np.float64).reshape(-1, 6), qpos, qvel,
+                 dt=float(model.opt.timestep), restitution=float(restitution), friction=float(friction),
                  gravity=np.array(model.opt.gravity, dtype=np.float64))
 
 
@@ -105,12 +137,13 @@ _worlds: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 _worlds_by_id: dict = {}
 
 
-def _scene_of(model) -> Scene:
+def _scene_of(model, restitution: float = 1.0, friction: float = 0.5) -> Scene:
     sc = getattr(model, "rb_scene", None)
-    return sc if sc is not None else scene_from_mujoco(model)
+    return sc if sc is not None else scene_from_mujoco(model, restitution, friction)
 
 
-def world_for(model, normal_convention: str = "oriented", law: str = "mujoco", tol: float = 0.01) -> World:
+def world_for(model, normal_convention: str = "oriented", law: str = "mujoco", tol: float = 0.01,
+              restitution: float = 1.0, friction: float = 0.5) -> World:
     """The cached GPU world of `model` (one per model and contact law)."""
     try:
         ws = _worlds.get(model)
@@ -124,10 +157,20 @@ def world_for(model, normal_convention: str = "oriented", law: str = "mujoco", t
             _worlds_by_id[id(model)] = ws
     w = ws.get(law)
     if w is None:
-        w = ws[law] = World(_scene_of(model), normal_convention=normal_convention, law=law, tol=tol)
+        w = ws[law] = World(_scene_of(model, restitution, friction), normal_convention=normal_convention,
+                            law=law, tol=tol)
     elif law == "balls" and w.tol != tol:
         w.set_contact_law(law, tol)
     return w
+
+
+def name2id(model, obj: str) -> int:
+    """mj_name2id(model, mjOBJ_BODY, obj): the SceneModel's own table, or
+    mujoco.mj_name2id for a real MjModel (collision.py:58)."""
+    if isinstance(model, SceneModel) or not hasattr(model, "body_jntnum"):
+        return model.name2id(obj) if hasattr(model, "name2id") else -1
+    mj = _mujoco()
+    return int(mj.mj_name2id(model, mj.mjtObj.mjOBJ_BODY, obj))
 
 
 def body_index(model, obj: str) -> int:
@@ -135,32 +178,34 @@ def body_index(model, obj: str) -> int:
     indexes model arrays with the raw id, so an unknown name (-1) selects the
     LAST body (single_sphere_bounce.py:67 passes "sphere" for the
     body "ball" and works by accident); reproduced, with a warning."""
-    nbody = getattr(model, "nbody", None)
-    bid = model.name2id(obj) if hasattr(model, "name2id") else -1
+    bid = name2id(model, obj)
     if bid < 0:
         warnings.warn(f"body {obj!r} not found: using the last body, as mj_name2id's -1 does "
                       f"in the reference (SURVEY D4)", stacklevel=3)
-        bid = nbody - 1
-    k = bid - SceneModel.FIRST
-    if k < 0:
+        bid = model.nbody - 1
+    fb = free_bodies(model)
+    if bid not in fb:
         raise ValueError(f"body {obj!r} is not a free body")
-    return k
+    return fb.index(bid)
 
 
 def step_model(model, data, nsteps: int, dt: float, restitution: float, friction: float,
                threshold: float, normal_convention: str = "oriented", law: str = "mujoco",
                tol: float = 0.01) -> None:
-    """Upload data's state, run nsteps reference steps on the GPU, write back."""
-    w = world_for(model, normal_convention, law, tol)
-    w.set_state(np.asarray(data.qpos).reshape(-1, 7), np.asarray(data.qvel).reshape(-1, 6))
+    """Upload data's state, run nsteps reference steps on the GPU, write back
+    (the free bodies' joints only, at their jnt_qposadr / jnt_dofadr)."""
+    w = world_for(model, normal_convention, law, tol, restitution, friction)
+    qi, vi = state_index(model)
+    qpos, qvel = np.asarray(data.qpos), np.asarray(data.qvel)
+    w.set_state(qpos[qi], qvel[vi])
     xf = np.asarray(getattr(data, "xfrc_applied", np.zeros((1, 6))))
-    first = getattr(model, "FIRST", SceneModel.FIRST)
-    xf_free = xf[first:first + w.scene.n] if xf.shape[0] >= first + w.scene.n else None
+    fb = free_bodies(model)
+    xf_free = xf[fb] if xf.shape[0] > max(fb) else None
     w.set_xfrc(xf_free if xf_free is not None and np.any(xf_free) else None)
     w.step(nsteps, dt=dt, restitution=restitution, friction=friction, threshold=threshold)
     q, v = w.get_state()
-    data.qpos[:] = q.reshape(-1)
-    data.qvel[:] = v.reshape(-1)
+    data.qpos[qi] = q
+    data.qvel[vi] = v
 
 
 def load_scene_model(scene: Scene):
@@ -171,4 +216,4 @@ def load_scene_model(scene: Scene):
 
 
 __all__ = ["SceneModel", "SceneData", "world_for", "step_model", "body_index", "load_scene_model",
-           "scene_from_mujoco", "GRAVITY"]
+           "scene_from_mujoco", "free_bodies", "state_index", "name2id", "GRAVITY"]

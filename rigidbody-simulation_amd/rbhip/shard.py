@@ -221,11 +221,18 @@ class ShardedWorld:
         q, v = self.world.get_state()
         if self.P == 1:
             return q, v
-        t = self.torch.from_numpy(np.concatenate([q, v], axis=1))
+        # each rank contributes its own rows [r*S, r*S + S) (padded to S):
+        # an all-gather moves the words unchanged (a sum would turn -0.0
+        # into +0.0), so the result is bit-identical to one World's state
+        n = q.shape[0]
+        S = -(-n // self.P)
+        lo, hi = min(self.rank * S, n), min(self.rank * S + S, n)
+        mine = np.zeros((S, 13))
+        mine[:hi - lo, :7], mine[:hi - lo, 7:] = q[lo:hi], v[lo:hi]
+        t = self.torch.from_numpy(mine)
         if self.dist.get_backend(self.group) == "nccl":
             t = t.to(f"cuda:{self.torch.cuda.current_device()}")
-        elif t.dtype != self.torch.float64:
-            t = t.double()
-        self.dist.all_reduce(t, group=self.group)      # rows are disjoint: sum == union
-        a = t.cpu().numpy()
+        parts = [self.torch.empty_like(t) for _ in range(self.P)]
+        self.dist.all_gather(parts, t, group=self.group)
+        a = self.torch.cat(parts).cpu().numpy()[:n]
         return a[:, :7].copy(), a[:, 7:].copy()

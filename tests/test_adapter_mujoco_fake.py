@@ -1,0 +1,131 @@
+"""rbhip.adapter against a real-MuJoCo-shaped model, on CPU.
+
+MuJoCo is not installed here, so `mujoco` is a duck-typed fake in
+sys.modules with the attributes the adapter reads (mj_name2id, mjtObj,
+mjtJoint, mjtGeom, MjData, mj_forward) and a model whose free joints do NOT
+start at qpos 0 (a hinge body comes first).  This pins the adapter's
+indexing (jnt_qposadr / jnt_dofadr, mj_name2id, caller e / mu —
+collision.py:58-61, multi_sphere_bounce.py:47-51), not MuJoCo itself: the
+real-MuJoCo path stays parity-unpinned."""
+import sys
+import types
+
+import numpy as np
+import pytest
+
+JNT_FREE, JNT_HINGE = 0, 3
+GEOM_PLANE, GEOM_SPHERE, GEOM_BOX = 0, 2, 6
+
+
+@pytest.fixture
+def fake_mujoco(monkeypatch):
+    mj = types.ModuleType("mujoco")
+    mj.mjtJoint = types.SimpleNamespace(mjJNT_FREE=JNT_FREE, mjJNT_HINGE=JNT_HINGE)
+    mj.mjtGeom = types.SimpleNamespace(mjGEOM_PLANE=GEOM_PLANE, mjGEOM_SPHERE=GEOM_SPHERE, mjGEOM_BOX=GEOM_BOX)
+    mj.mjtObj = types.SimpleNamespace(mjOBJ_BODY=1)
+
+    def mj_name2id(model, objtype, name):
+        assert objtype == 1
+        return model.body_names.index(name) if name in model.body_names else -1
+
+    class MjData:
+        def __init__(self, model):
+            self.qpos = model.qpos0.copy()
+            self.qvel = np.arange(model.nv, dtype=np.float64) * 0.5
+            self.xfrc_applied = np.zeros((model.nbody, 6))
+            self.geom_xmat = np.tile(np.eye(3).reshape(-1), (model.ngeom, 1))
+            self.geom_xpos = np.zeros((model.ngeom, 3))
+
+    mj.mj_name2id = mj_name2id
+    mj.MjData = MjData
+    mj.mj_forward = lambda model, data: None
+    monkeypatch.setitem(sys.modules, "mujoco", mj)
+    return mj
+
+
+class FakeModel:
+    """world (0), a hinged arm (1: qpos 0, dof 0), plane body (2), ball (3:
+    free, qpos 1..7, dof 1..6), box (4: free, qpos 8..14, dof 7..12)."""
+
+    def __init__(self):
+        self.body_names = ["world", "arm", "floor", "ball", "box"]
+        self.nbody = 5
+        self.body_jntnum = np.array([0, 1, 0, 1, 1])
+        self.body_jntadr = np.array([-1, 0, -1, 1, 2])
+        self.jnt_type = np.array([JNT_HINGE, JNT_FREE, JNT_FREE])
+        self.jnt_qposadr = np.array([0, 1, 8])
+        self.jnt_dofadr = np.array([0, 1, 7])
+        self.nq, self.nv = 15, 13
+        self.body_mass = np.array([0.0, 1.0, 0.0, 0.2, 25.6])
+        self.body_inertia = np.array([[0, 0, 0], [1, 1, 1], [0, 0, 0], [8e-4] * 3, [2.73] * 3], dtype=float)
+        self.ngeom = 3
+        self.geom_type = np.array([GEOM_PLANE, GEOM_SPHERE, GEOM_BOX])
+        self.geom_bodyid = np.array([2, 3, 4])
+        self.geom_size = np.array([[5, 5, 0.1], [0.1, 0, 0], [0.4, 0.4, 0.4]], dtype=float)
+        self.opt = types.SimpleNamespace(timestep=0.009, gravity=np.array([0, 0, -9.8]))
+        self.qpos0 = np.concatenate([[0.3], [0, 0, 1.0, 1, 0, 0, 0], [2.0, 0, 0.5, 1, 0, 0, 0]])
+
+
+def test_free_bodies_and_state_index(fake_mujoco):
+    from rbhip import adapter
+    m = FakeModel()
+    assert adapter.free_bodies(m) == [3, 4]
+    qi, vi = adapter.state_index(m)
+    assert qi.tolist() == [list(range(1, 8)), list(range(8, 15))]
+    assert vi.tolist() == [list(range(1, 7)), list(range(7, 13))]
+
+
+def test_body_index_uses_mj_name2id(fake_mujoco):
+    from rbhip import adapter
+    m = FakeModel()
+    assert adapter.body_index(m, "ball") == 0 and adapter.body_index(m, "box") == 1
+    with pytest.warns(UserWarning, match="last body"):
+        assert adapter.body_index(m, "sphere") == 1          # -1 -> last body
+    with pytest.raises(ValueError, match="not a free body"):
+        adapter.body_index(m, "arm")
+
+
+def test_scene_from_mujoco_takes_caller_law(fake_mujoco):
+    from rbhip import adapter
+    from rbhip.scenes import BOX, SPHERE
+    m = FakeModel()
+    sc = adapter.scene_from_mujoco(m, restitution=0.2, friction=0.6)
+    assert sc.restitution == 0.2 and sc.friction == 0.6 and sc.dt == 0.009
+    assert sc.kind.tolist() == [SPHERE, BOX]
+    assert np.array_equal(sc.mass, [0.2, 25.6])
+    assert np.array_equal(sc.qpos0, m.qpos0[1:].reshape(2, 7))
+    assert np.array_equal(sc.planes, [[0, 0, 1, 0, 0, 0]])
+
+
+def test_step_model_writes_free_joints_only(fake_mujoco, monkeypatch):
+    """step_model gathers the free bodies' qpos / qvel at their addresses and
+    scatters the stepped state back, leaving the hinge untouched (a stand-in
+    world adds 1 to every value: no GPU here)."""
+    from rbhip import adapter
+    m = FakeModel()
+    d = fake_mujoco.MjData(m)
+    seen = {}
+
+    class StandIn:
+        scene = None
+
+        def set_state(self, q, v):
+            seen["q"], seen["v"] = q.copy(), v.copy()
+
+        def set_xfrc(self, xf):
+            seen["xf"] = xf
+
+        def step(self, n, **kw):
+            seen["kw"] = kw
+
+        def get_state(self):
+            return seen["q"] + 1.0, seen["v"] + 1.0
+
+    monkeypatch.setattr(adapter, "world_for", lambda *a, **k: StandIn())
+    q0, v0 = d.qpos.copy(), d.qvel.copy()
+    adapter.step_model(m, d, 1, 0.009, 0.2, 0.6, 1e-4)
+    assert np.array_equal(seen["q"], q0[1:].reshape(2, 7)) and np.array_equal(seen["v"], v0[1:].reshape(2, 6))
+    assert seen["kw"] == dict(dt=0.009, restitution=0.2, friction=0.6, threshold=1e-4)
+    assert d.qpos[0] == q0[0] and d.qvel[0] == v0[0]
+    assert np.array_equal(d.qpos[1:], q0[1:] + 1.0) and np.array_equal(d.qvel[1:], v0[1:] + 1.0)
+    assert seen["xf"] is None

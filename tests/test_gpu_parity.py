@@ -84,21 +84,83 @@ def _oracle_run(oracle, sc, steps, dtype="f64", record=False):
     return oracle.step(osc, sc.qpos0, sc.qvel0, steps, dtype=dtype, record=record)
 
 
-@pytest.mark.parametrize("cfg,steps", [("c2", 300), ("c4", 40), ("c5", 120)])
-def test_config_trajectory_bit_exact_vs_oracle(rb, oracle, cfg, steps):
-    from rbhip import scenes
-    sc = scenes.make(cfg)
-    q0, v0, (cnt, par, kin, dis) = _oracle_run(oracle, sc, steps, record=True)
-    with rb.World(sc) as w:
-        w.step(steps - 1)                 # graph path
-        w.record_contacts(True)
-        w.step(1)                         # single-launch path, recorded
-        q, v = w.get_state()
+@pytest.fixture
+def oracle16(oracle):
+    """The oracle on 16 OpenMP threads (the GPU box's host-core share)."""
+    oracle.set_threads(16)
+    yield oracle
+    oracle.set_threads(1)
+
+
+def _same(a, b):
+    """Bit identity as 64-bit words (the sign of zeros counts)."""
+    return a.shape == b.shape and np.array_equal(np.ascontiguousarray(a).view(np.uint64),
+                                                 np.ascontiguousarray(b).view(np.uint64))
+
+
+def _check_window(w, oracle, osc, q, v, first, last, tag):
+    """Steps first..last (1-based, from t = 0) one launch at a time, each
+    recorded: contact lists and state bit-exact with the oracle stepping
+    the same state.  Returns the state after `last` and the number of
+    sphere-sphere contacts seen."""
+    w.record_contacts(True)
+    ss = 0
+    for t in range(first, last + 1):
+        q, v, (cnt, par, kin, dis) = oracle.step(osc, q, v, 1, record=True)
+        w.step(1)
         gc, gp, gk, gd = w.contacts()
-    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
-    assert np.array_equal(gd, dis)
-    assert np.array_equal(q, q0) and np.array_equal(v, v0)
-    assert (kin == 16).any() or cfg != "c2"          # C2 exercises sphere-sphere contacts
+        assert np.array_equal(gc, cnt), f"{tag}: contact counts differ at step {t}"
+        assert np.array_equal(gp, par) and np.array_equal(gk, kin), f"{tag}: contact partners/kinds differ at step {t}"
+        assert _same(gd, dis), f"{tag}: contact distances differ at step {t}"
+        gq, gv = w.get_state()
+        assert _same(gq, q) and _same(gv, v), f"{tag}: state differs after step {t}"
+        ss += int((kin == 16).sum())
+    w.record_contacts(False)
+    return q, v, ss
+
+
+def test_c3_bench_windows_bit_exact(rb, oracle16):
+    """The bench scene (C3, 65,536 spheres, the wide step form) from t = 0
+    for 500 steps, graph-replayed between two recorded windows: the
+    driver's timed window (steps 25-45: --warmup 5, K = 20) and steps
+    480-500 — every recorded step's contacts and state bit-exact with the
+    oracle, sphere-sphere contacts present in both windows."""
+    from rbhip import scenes
+    oracle = oracle16
+    sc = scenes.make("c3")
+    osc = oracle.OracleScene(sc)
+    with rb.World(sc) as w:
+        assert w.n_owned == 65536
+        q, v = oracle.step(osc, sc.qpos0, sc.qvel0, 24)
+        w.step(24)
+        q, v, ss1 = _check_window(w, oracle, osc, q, v, 25, 45, "c3")
+        q, v = oracle.step(osc, q, v, 479 - 45)
+        w.step(479 - 45)
+        q, v, ss2 = _check_window(w, oracle, osc, q, v, 480, 500, "c3")
+    assert ss1 > 0 and ss2 > 1000, (ss1, ss2)
+
+
+@pytest.mark.parametrize("cfg,steps,every", [("c2", 2000, 500), ("c4", 400, 100), ("c5", 1000, 250)])
+def test_config_long_run_bit_exact_vs_oracle(rb, oracle16, cfg, steps, every):
+    """C2 for the survey's 2,000 steps, C4 (65,536 spheres on the incline,
+    friction-dominated) for 400, C5 (16,384 cubes) for 1,000: state bit-exact
+    with the oracle at every checkpoint (graph-replayed chunks) and the last
+    step's contact lists bit-exact."""
+    from rbhip import scenes
+    oracle = oracle16
+    sc = scenes.make(cfg)
+    osc = oracle.OracleScene(sc)
+    q, v = sc.qpos0, sc.qvel0
+    with rb.World(sc) as w:
+        for t in range(0, steps - every, every):
+            q, v = oracle.step(osc, q, v, every)
+            w.step(every)
+            gq, gv = w.get_state()
+            assert _same(gq, q) and _same(gv, v), f"{cfg}: state differs after step {t + every}"
+        q, v = oracle.step(osc, q, v, every - 1)
+        w.step(every - 1)
+        q, v, ss = _check_window(w, oracle, osc, q, v, steps, steps, cfg)
+    assert ss > 0 or cfg != "c2"          # C2 exercises sphere-sphere contacts
 
 
 def test_c3_one_step_parity_from_evolved_state(rb, oracle):

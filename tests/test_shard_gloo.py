@@ -1,5 +1,6 @@
 """Body-range sharding over torch.distributed (gloo, world_size 2 and 3) on
-CPU: the real ShardedWorld exchange logic ([P][3][S] position layout, in-rank
+CPU: the real ShardedWorld exchange logic (the library's [P][S][4] snapshot
+layout — x, y, z, bounding radius per body in global id order — in-rank
 slice, all-gather, publish), with the per-rank stepper emulated by the
 oracle (test-only stand-in for librbhip's rb_shard_step /
 rb_shard_exchange_done).  Result must be bit-identical to one rank."""
@@ -29,25 +30,27 @@ class OracleShardStepper:
         self.lo, self.hi = rank * self.S, min(rank * self.S + self.S, scene.n)
         self.q = scene.qpos0.copy()
         self.v = scene.qvel0.copy()
-        self.buf = torch.zeros(P * 3 * self.S, dtype=torch.float64)
-        g = self.buf.view(P, 3, self.S)
+        # rb_internal.hpp Snap<T>{x, y, z, r}, [P][S][4] (rb_gpos_buffer)
+        self.buf = torch.zeros(P * self.S * 4, dtype=torch.float64)
+        g = self.buf.view(P, self.S, 4)
         for b in range(scene.n):
-            g[b // self.S, :, b % self.S] = torch.from_numpy(self.q[b, 0:3])
+            g[b // self.S, b % self.S, 0:3] = torch.from_numpy(self.q[b, 0:3])
+            g[b // self.S, b % self.S, 3] = float(scene.size[b, 0])
 
     def exchange_buffer(self, torch_mod):
-        return self.buf, 3 * self.S
+        return self.buf, 4 * self.S
 
     def shard_step(self, **params):
         q, v = self.O.step(self.osc, self.q, self.v, 1)
         self.q[self.lo:self.hi], self.v[self.lo:self.hi] = q[self.lo:self.hi], v[self.lo:self.hi]
-        g = self.buf.view(self.P, 3, self.S)
-        g[self.rank, :, : self.hi - self.lo] = torch.from_numpy(self.q[self.lo:self.hi, 0:3].T.copy())
+        g = self.buf.view(self.P, self.S, 4)
+        g[self.rank, : self.hi - self.lo, 0:3] = torch.from_numpy(self.q[self.lo:self.hi, 0:3].copy())
 
     def shard_exchange_done(self):
-        g = self.buf.view(self.P, 3, self.S).numpy()
+        g = self.buf.view(self.P, self.S, 4).numpy()
         for b in range(self.sc.n):
             if not (self.lo <= b < self.hi):
-                self.q[b, 0:3] = g[b // self.S, :, b % self.S]
+                self.q[b, 0:3] = g[b // self.S, b % self.S, 0:3]
 
     def sync(self):
         pass
@@ -94,7 +97,9 @@ def test_sharded_exchange_is_p_invariant(tmp_path, oracle, P):
     out = str(tmp_path / "state.npy")
     mp.start_processes(_worker, args=(P, _free_port(), steps, out), nprocs=P, start_method="spawn")
     got = np.load(out)
-    assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
+    # compared as 64-bit words: the gather must keep the sign of zeros
+    assert np.array_equal(got[:, :7].view(np.uint64), q1.view(np.uint64))
+    assert np.array_equal(got[:, 7:].view(np.uint64), v1.view(np.uint64))
 
 
 def test_tiled_scene_ownership():
@@ -108,3 +113,23 @@ def test_tiled_scene_ownership():
         xs = sc.qpos0[r * S:(r + 1) * S, 0]
         if r > 0:
             assert xs.min() > sc.qpos0[(r - 1) * S:r * S, 0].max()
+
+
+def test_strong_scene_ownership():
+    """bench.py's default (strong scaling): the one C3 scene split by body-id
+    range; ids run row-major, so rank r's range is the r-th y-slab of
+    256 / P grid rows."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from rbhip import scenes
+    for P in (1, 2, 4, 8):
+        sc, desc = bench.make_scene("c3", P, "strong")
+        assert sc.n == 65536 and np.array_equal(sc.qpos0, scenes.make("c3").qpos0)
+        S = -(-sc.n // P)
+        for r in range(1, P):
+            assert sc.qpos0[r * S:(r + 1) * S, 1].min() > sc.qpos0[(r - 1) * S:r * S, 1].max()
+        assert ("strong" in desc) == (P > 1)
+    sc, desc = bench.make_scene("c4", 8, "weak")
+    assert sc.n == 8 * 65536 and "weak" in desc
