@@ -39,7 +39,7 @@ extern "C" {
 #define RB_ENOMEM      (-12)  /* device or host allocation failed               */
 #define RB_ENODEV      (-19)  /* no HIP device / HIP runtime failure            */
 #define RB_EOVERFLOW   (-75)  /* contact or broadphase-bucket capacity exceeded */
-#define RB_EUNSUPPORTED (-95) /* box-box / box-sphere contact (not restated)    */
+#define RB_EUNSUPPORTED (-95) /* unsupported combination (e.g. box pairs across shards) */
 #define RB_EDOM        (-33)  /* non-finite or out-of-range body position       */
 
 /* ---- enums ------------------------------------------------------------- */
@@ -64,6 +64,9 @@ extern "C" {
 #define RB_CK_PLANE_SPHERE   0
 #define RB_CK_PLANE_BOX0     1   /* 1 + corner index (0..7, corner bits i&1,i&2,i&4) */
 #define RB_CK_SPHERE_SPHERE 16
+#define RB_CK_SPHERE_BOX    17   /* sphere = geom1 (MuJoCo dispatches by geom type) */
+#define RB_CK_BOX_BOX0      32   /* 32 + k: k-th face-clip point of a box pair (k < 4) */
+#define RB_CK_BOX_EDGE      40   /* edge-edge point of a box pair */
 
 /* ---- scene descriptor -------------------------------------------------- */
 typedef struct rb_scene_desc {
@@ -214,8 +217,11 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol);
 /* ---- parity support ---------------------------------------------------- */
 /* Record the contact list generated during the most recent step (off by
  * default: recording costs HBM traffic).  Canonical per-body order: plane
- * contacts (plane order; box corners in bit order), then sphere partners by
- * ascending body id.  Output is CSR over the owned bodies: counts[n_owned];
+ * contacts (plane order; box corners in bit order), then partners by
+ * ascending body id (a box-involved partner: its contacts in generation
+ * order, RB_CK_SPHERE_BOX / RB_CK_BOX_BOX0 + k / RB_CK_BOX_EDGE).  Box-
+ * involved pairs are solved in unsharded worlds; a sharded world reports
+ * one within contact range as RB_EUNSUPPORTED.  Output is CSR over the owned bodies: counts[n_owned];
  * partner (body id, or -1-plane_index), kind (RB_CK_*), dist.  cap is the
  * capacity of the flat arrays; total receives the number of records. */
 int rb_record_contacts(rb_world *w, int enable);
@@ -239,6 +245,14 @@ int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in,
  * (ball_collision.py:53-68). */
 int rb_kat_pair_impulse(int32_t device, int32_t dtype, int64_t n, const double *in,
                         double *out);
+/* rb_kat_narrow: the box-involved narrowphase (this
+ * project's restatement of MuJoCo's sphere-box / box-box primitives, which
+ * are not available offline — parity against MuJoCo is unpinned):
+ * per case in[22] = kind1, kind2 (RB_BODY_*), c1[3], q1[4] (wxyz), size1[3],
+ * c2[3], q2[4], size2[3] (body 1 = the lower id) -> out[33] = count, then
+ * per contact dist, pos[3], frame[3] (geom1 -> geom2; a sphere is geom1 of
+ * a sphere-box pair), kind (RB_CK_*). */
+int rb_kat_narrow(int32_t device, int32_t dtype, int64_t n, const double *in, double *out);
 /* rb_kat_apply: apply_impulse_friction alone (physics_utils.py:25-49) with
  * caller-given impulses: in[26] = m, v[3], w[3], r[3], n[3], jn, jt[3],
  * inertia_world[9] -> out[6] = v'[3], w'[3]. */

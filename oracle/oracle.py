@@ -55,6 +55,7 @@ def lib():
                                                       C.c_double, C.c_double, P, P, P, P, C.c_int64, P]
             getattr(L, f"rbo_contacts_{sfx}").argtypes = [P, P, P, P, P, P, P, P, C.c_int64, P]
             getattr(L, f"rbo_kat_pair_impulse_{sfx}").argtypes = [C.c_int64, P, P]
+            getattr(L, f"rbo_kat_narrow_{sfx}").argtypes = [C.c_int64, P, P]
             getattr(L, f"rbo_pair_step_{sfx}").argtypes = [P, P, P, C.c_int64, C.c_double, C.c_double,
                                                            C.c_double, C.c_double, P, P, C.c_int64, P]
         L.rbo_set_threads.argtypes = [C.c_int]
@@ -98,7 +99,10 @@ class OracleScene:
         for k in range(3):
             d.gravity[k] = float(sc.gravity[k])
         self.desc = d
-        self.maxrec = 4 * d.n_planes + max_partners
+        # records per body (rb_oracle_impl.h contact_stride): 4 per plane, 1 per
+        # sphere partner, 4 per partner when the scene has boxes
+        boxes = bool(np.any(self.kind != 0))
+        self.maxrec = 4 * d.n_planes + (4 if boxes else 1) * max_partners
 
 
 def kat_impulse(inp: np.ndarray, dtype: str = "f64") -> np.ndarray:
@@ -163,6 +167,17 @@ def contacts(osc: OracleScene, qpos, dtype: str = "f64"):
         raise RuntimeError(f"oracle rbo_contacts failed: {RB_ENAMES.get(rc, rc)}")
     t = tot.value
     return cnt, par[:t], kin[:t], dis[:t], pos[:t], frm[:t]
+
+
+def kat_narrow(inp: np.ndarray, dtype: str = "f64") -> np.ndarray:
+    """Box-pair narrowphase (rb_oracle_impl.h sphere_box / box_box, this
+    project's definition; MuJoCo unpinned) per row of in[22] = kind1, kind2,
+    c1, q1, s1, c2, q2, s2 (body 1 = lower id) -> out[33] = count, then per
+    contact dist, pos[3], frame[3], kind."""
+    inp = np.ascontiguousarray(inp, np.float64)
+    out = np.zeros((inp.shape[0], 33))
+    getattr(lib(), f"rbo_kat_narrow_{dtype}")(inp.shape[0], _ptr(inp), _ptr(out))
+    return out
 
 
 def kat_pair_impulse(inp: np.ndarray, dtype: str = "f64") -> np.ndarray:

@@ -237,6 +237,7 @@ static void FN(mj_body_mat)(const REAL qin[4], REAL M[9]) {
 typedef struct {
     int32_t partner;   /* body id, or -1 - plane */
     int32_t kind;      /* RB_CK_* */
+    int32_t self_g1;   /* the body being solved is geom1 (ORIENTED flips the normal) */
     REAL dist;
     REAL pos[3];
     REAL frame[3];     /* MuJoCo contact normal, geom1 -> geom2 */
@@ -297,6 +298,279 @@ static int FN(sphere_sphere)(const REAL c1[3], REAL r1, const REAL c2[3], REAL r
     for (int k = 0; k < 3; ++k) { con->pos[k] = f[k] * s + c1[k]; con->frame[k] = f[k]; }
     con->kind = RB_CK_SPHERE_SPHERE;
     return 1;
+}
+
+/* ---------------- box pairs ---------------------------
+ * MuJoCo's mjc_SphereBox and mjc_BoxBox are third-party C that is neither
+ * installed nor vendored here, so these are THIS PROJECT'S DEFINITIONS,
+ * following the published structure of those primitives (margin 0):
+ *   sphere-box: the sphere centre in the box frame is clamped to the box;
+ *     outside: normal = clamped - centre (sphere -> box), dist = |.| - r,
+ *     pos = midpoint of the clamped point and the sphere's deepest point;
+ *     centre inside: the nearest face (faces +x, -x, +y, -y, +z, -z,
+ *     first minimum), dist = -(face distance + r).  Sphere = geom1.
+ *   box-box: separating-axis test over the 15 axes (A faces, B faces, the 9
+ *     edge crosses; an edge axis wins only if 1.05 x its separation beats
+ *     the best face axis), normal oriented geom1 -> geom2.  Face axis: the
+ *     incident face of the other box (most anti-parallel normal) is clipped
+ *     against the reference face rectangle (Sutherland-Hodgman, planes
+ *     +a1, -a1, +a2, -a2); clipped points below the reference face are
+ *     contacts (at most 4: the 4 deepest, kept in polygon order), pos
+ *     halfway between the faces.  Edge axis: one contact at the midpoint of
+ *     the closest points of the two supporting edges, dist = the separation.
+ * Parity against MuJoCo itself is UNPINNED; the HIP path (csrc/rb_boxes.hpp)
+ * must match these bit for bit. */
+static void FN(mat_col)(const REAL M[9], int k, REAL u[3]) { u[0] = M[k]; u[1] = M[3 + k]; u[2] = M[6 + k]; }
+static inline REAL FN(clampv)(REAL x, REAL lo, REAL hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* sphere (c1, r1) = geom1, box (c2, M2, h2) = geom2 */
+static int FN(sphere_box)(const REAL c1[3], REAL r1, const REAL c2[3], const REAL M2[9], const REAL h2[3],
+                          FN(rbo_contact) *con) {
+    REAL tmp[3], center[3], clamped[3], nearest[3], pos[3], nrm[3];
+    for (int k = 0; k < 3; ++k) tmp[k] = c1[k] - c2[k];
+    for (int k = 0; k < 3; ++k) center[k] = M2[k] * tmp[0] + M2[3 + k] * tmp[1] + M2[6 + k] * tmp[2];
+    for (int k = 0; k < 3; ++k) clamped[k] = FN(clampv)(center[k], -h2[k], h2[k]);
+    for (int k = 0; k < 3; ++k) nearest[k] = clamped[k] - center[k];
+    const REAL dist = SQRT(FN(mj_dot3)(nearest, nearest));
+    if (dist - r1 > (REAL)0) return 0;
+    REAL cd;
+    if (dist <= (REAL)1e-15) {
+        REAL closest = (REAL)2 * ((h2[0] + h2[1]) + h2[2]);
+        int kf = 0;
+        for (int i = 0; i < 6; ++i) {
+            const int a = i / 2;
+            const REAL df = (i % 2 == 0) ? h2[a] - center[a] : h2[a] + center[a];
+            if (df < closest) { closest = df; kf = i; }
+        }
+        const int a = kf / 2;
+        const REAL s = (kf % 2 == 0) ? (REAL)1 : (REAL)-1;
+        for (int k = 0; k < 3; ++k) { nrm[k] = (REAL)0; pos[k] = center[k]; }
+        nrm[a] = -s;
+        pos[a] = center[a] + s * ((closest - r1) / (REAL)2);
+        cd = -closest - r1;
+    } else {
+        const REAL inv = (REAL)1 / dist;
+        for (int k = 0; k < 3; ++k) nrm[k] = nearest[k] * inv;
+        for (int k = 0; k < 3; ++k) pos[k] = (clamped[k] + (center[k] + nrm[k] * r1)) * (REAL)0.5;
+        cd = dist - r1;
+    }
+    for (int k = 0; k < 3; ++k) {
+        con->pos[k] = (M2[3 * k] * pos[0] + M2[3 * k + 1] * pos[1] + M2[3 * k + 2] * pos[2]) + c2[k];
+        con->frame[k] = M2[3 * k] * nrm[0] + M2[3 * k + 1] * nrm[1] + M2[3 * k + 2] * nrm[2];
+    }
+    con->dist = cd;
+    con->kind = RB_CK_SPHERE_BOX;
+    return 1;
+}
+
+/* box A (pa, Ma, ha) = geom1, box B = geom2; up to 4 contacts into con */
+static int FN(box_box)(const REAL pa[3], const REAL Ma[9], const REAL ha[3], const REAL pb[3], const REAL Mb[9],
+                       const REAL hb[3], FN(rbo_contact) *con) {
+    REAL ua[3][3], ub[3][3], d[3], R[3][3], AR[3][3], da[3], db[3];
+    for (int i = 0; i < 3; ++i) { FN(mat_col)(Ma, i, ua[i]); FN(mat_col)(Mb, i, ub[i]); }
+    for (int k = 0; k < 3; ++k) d[k] = pb[k] - pa[k];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) { R[i][j] = FN(mj_dot3)(ua[i], ub[j]); AR[i][j] = FABS(R[i][j]); }
+    for (int i = 0; i < 3; ++i) { da[i] = FN(mj_dot3)(d, ua[i]); db[i] = FN(mj_dot3)(d, ub[i]); }
+    REAL best = (REAL)0, L[3] = {0, 0, 0}, dL = 0;
+    int bk = -1;
+    for (int i = 0; i < 3; ++i) {
+        const REAL s = FABS(da[i]) - (ha[i] + ((hb[0] * AR[i][0] + hb[1] * AR[i][1]) + hb[2] * AR[i][2]));
+        if (s > (REAL)0) return 0;
+        if (bk < 0 || s > best) { best = s; bk = i; }
+    }
+    for (int j = 0; j < 3; ++j) {
+        const REAL s = FABS(db[j]) - (((ha[0] * AR[0][j] + ha[1] * AR[1][j]) + ha[2] * AR[2][j]) + hb[j]);
+        if (s > (REAL)0) return 0;
+        if (s > best) { best = s; bk = 3 + j; }
+    }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const REAL *a = ua[i], *b = ub[j];
+            REAL c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+            const REAL len = SQRT(FN(mj_dot3)(c, c));
+            if (len < (REAL)1e-6) continue;                       /* parallel edges */
+            const REAL inv = (REAL)1 / len;
+            for (int k = 0; k < 3; ++k) c[k] = c[k] * inv;
+            const REAL pA = (ha[0] * FABS(FN(mj_dot3)(ua[0], c)) + ha[1] * FABS(FN(mj_dot3)(ua[1], c))) +
+                            ha[2] * FABS(FN(mj_dot3)(ua[2], c));
+            const REAL pB = (hb[0] * FABS(FN(mj_dot3)(ub[0], c)) + hb[1] * FABS(FN(mj_dot3)(ub[1], c))) +
+                            hb[2] * FABS(FN(mj_dot3)(ub[2], c));
+            const REAL dc = FN(mj_dot3)(d, c);
+            const REAL s = FABS(dc) - (pA + pB);
+            if (s > (REAL)0) return 0;
+            if (s * (REAL)1.05 > best) { best = s; bk = 6 + 3 * i + j; L[0] = c[0]; L[1] = c[1]; L[2] = c[2]; dL = dc; }
+        }
+    if (bk < 3) { for (int k = 0; k < 3; ++k) L[k] = ua[bk][k]; dL = da[bk]; }
+    else if (bk < 6) { for (int k = 0; k < 3; ++k) L[k] = ub[bk - 3][k]; dL = db[bk - 3]; }
+    REAL n[3];
+    for (int k = 0; k < 3; ++k) n[k] = dL < (REAL)0 ? -L[k] : L[k];
+
+    if (bk >= 6) {                                                /* edge - edge */
+        const int i = (bk - 6) / 3, j = (bk - 6) % 3;
+        REAL qa[3] = {pa[0], pa[1], pa[2]}, qb[3] = {pb[0], pb[1], pb[2]}, r[3];
+        for (int k = 0; k < 3; ++k) {
+            if (k == i) continue;
+            const REAL sg = FN(mj_dot3)(ua[k], n) > (REAL)0 ? ha[k] : -ha[k];
+            for (int c = 0; c < 3; ++c) qa[c] = qa[c] + ua[k][c] * sg;
+        }
+        for (int k = 0; k < 3; ++k) {
+            if (k == j) continue;
+            const REAL sg = FN(mj_dot3)(ub[k], n) > (REAL)0 ? -hb[k] : hb[k];
+            for (int c = 0; c < 3; ++c) qb[c] = qb[c] + ub[k][c] * sg;
+        }
+        for (int k = 0; k < 3; ++k) r[k] = qb[k] - qa[k];
+        const REAL a = R[i][j], e = FN(mj_dot3)(ua[i], r), f = FN(mj_dot3)(ub[j], r);
+        const REAL den = (REAL)1 - a * a;
+        const REAL s = FN(clampv)((e - a * f) / den, -ha[i], ha[i]);
+        const REAL t = FN(clampv)((a * e - f) / den, -hb[j], hb[j]);
+        for (int k = 0; k < 3; ++k) {
+            con->pos[k] = ((qa[k] + ua[i][k] * s) + (qb[k] + ub[j][k] * t)) * (REAL)0.5;
+            con->frame[k] = n[k];
+        }
+        con->dist = best;
+        con->kind = RB_CK_BOX_EDGE;
+        return 1;
+    }
+
+    /* face: reference box (the axis's owner), incident box (the other) */
+    const int refa = bk < 3, ra = refa ? bk : bk - 3;
+    const REAL *pr = refa ? pa : pb, *pi = refa ? pb : pa, *hr = refa ? ha : hb, *hi = refa ? hb : ha;
+    REAL (*ur)[3] = refa ? ua : ub, (*ui)[3] = refa ? ub : ua;
+    REAL nr[3], cdot[3], cinc[3], e1[3], e2[3], cref[3];
+    for (int k = 0; k < 3; ++k) nr[k] = refa ? n[k] : -n[k];    /* reference face normal, toward the incident box */
+    int kk = 0;
+    REAL cb = (REAL)-1;
+    for (int k = 0; k < 3; ++k) {
+        cdot[k] = FN(mj_dot3)(ui[k], nr);
+        if (FABS(cdot[k]) > cb) { cb = FABS(cdot[k]); kk = k; }
+    }
+    const REAL sg = cdot[kk] > (REAL)0 ? (REAL)-1 : (REAL)1;
+    const int b1 = kk == 0 ? 1 : 0, b2 = kk == 2 ? 1 : 2;
+    const int a1 = ra == 0 ? 1 : 0, a2 = ra == 2 ? 1 : 2;
+    for (int k = 0; k < 3; ++k) {
+        cinc[k] = pi[k] + ui[kk][k] * (sg * hi[kk]);
+        e1[k] = ui[b1][k] * hi[b1];
+        e2[k] = ui[b2][k] * hi[b2];
+        cref[k] = pr[k] + nr[k] * hr[ra];
+    }
+    REAL P[8][3], Q[8][3];
+    int np = 4;
+    for (int v = 0; v < 4; ++v) {                                 /* (+,+) (-,+) (-,-) (+,-) */
+        REAL vert[3], rel[3];
+        for (int k = 0; k < 3; ++k) {
+            vert[k] = (v == 0 || v == 3) ? cinc[k] + e1[k] : cinc[k] - e1[k];
+            vert[k] = (v < 2) ? vert[k] + e2[k] : vert[k] - e2[k];
+            rel[k] = vert[k] - cref[k];
+        }
+        P[v][0] = FN(mj_dot3)(rel, ur[a1]);
+        P[v][1] = FN(mj_dot3)(rel, ur[a2]);
+        P[v][2] = FN(mj_dot3)(rel, nr);
+    }
+    for (int pl = 0; pl < 4 && np > 0; ++pl) {
+        const int c = pl < 2 ? 0 : 1, neg = pl & 1;
+        const REAL w = pl < 2 ? hr[a1] : hr[a2];
+        int nq = 0;
+        for (int t = 0; t < np; ++t) {
+            const REAL *cur = P[t], *prv = P[(t + np - 1) % np];
+            const REAL fc = (neg ? -cur[c] : cur[c]) - w;
+            const REAL fp = (neg ? -prv[c] : prv[c]) - w;
+            const int ins = fc <= (REAL)0, pins = fp <= (REAL)0;
+            if (ins != pins && nq < 8) {                          /* the edge crosses the plane */
+                const REAL tt = fp / (fp - fc);
+                for (int k = 0; k < 3; ++k) Q[nq][k] = prv[k] + (cur[k] - prv[k]) * tt;
+                ++nq;
+            }
+            if (ins && nq < 8) { for (int k = 0; k < 3; ++k) Q[nq][k] = cur[k]; ++nq; }
+        }
+        for (int t = 0; t < nq; ++t) for (int k = 0; k < 3; ++k) P[t][k] = Q[t][k];
+        np = nq;
+    }
+    unsigned keep = 0;
+    int nk = 0;
+    for (int t = 0; t < np; ++t) if (P[t][2] <= (REAL)0) { keep |= 1u << t; ++nk; }
+    if (nk > 4) {                                                 /* the 4 deepest */
+        unsigned pick = 0;
+        for (int r = 0; r < 4; ++r) {
+            int bt = -1;
+            for (int t = 0; t < np; ++t)
+                if (((keep & ~pick) >> t) & 1u) if (bt < 0 || P[t][2] < P[bt][2]) bt = t;
+            pick |= 1u << bt;
+        }
+        keep = pick;
+    }
+    int m = 0;
+    for (int t = 0; t < np; ++t) {
+        if (!((keep >> t) & 1u)) continue;
+        const REAL x = P[t][0], y = P[t][1], z = P[t][2], s = -z / (REAL)2;
+        for (int k = 0; k < 3; ++k) {
+            const REAL wp = ((cref[k] + ur[a1][k] * x) + ur[a2][k] * y) + nr[k] * z;
+            con[m].pos[k] = wp + nr[k] * s;
+            con[m].frame[k] = n[k];
+        }
+        con[m].dist = z;
+        con[m].kind = RB_CK_BOX_BOX0 + m;
+        ++m;
+    }
+    return m;
+}
+
+/* The contacts of the pair (i, j) in MuJoCo's geom order — spheres by id,
+ * sphere before box, boxes by id — into con (at most 4); self_g1 marks
+ * whether body i is geom1. */
+static int FN(pair_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL *quat, int64_t i, int64_t j,
+                             FN(rbo_contact) *con) {
+    const int si = d->kind[i] == RB_BODY_SPHERE, sj = d->kind[j] == RB_BODY_SPHERE;
+    int64_t g1, g2;
+    if (si != sj) { g1 = si ? i : j; g2 = si ? j : i; }
+    else { g1 = i < j ? i : j; g2 = i < j ? j : i; }
+    int nc;
+    if (si && sj) {
+        nc = FN(sphere_sphere)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2, (REAL)d->size[3 * g2], con);
+    } else if (si != sj) {
+        REAL M[9], h[3] = {(REAL)d->size[3 * g2], (REAL)d->size[3 * g2 + 1], (REAL)d->size[3 * g2 + 2]};
+        FN(mj_body_mat)(quat + 4 * g2, M);
+        nc = FN(sphere_box)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2, M, h, con);
+    } else {
+        REAL M1[9], M2[9];
+        REAL h1[3] = {(REAL)d->size[3 * g1], (REAL)d->size[3 * g1 + 1], (REAL)d->size[3 * g1 + 2]};
+        REAL h2[3] = {(REAL)d->size[3 * g2], (REAL)d->size[3 * g2 + 1], (REAL)d->size[3 * g2 + 2]};
+        FN(mj_body_mat)(quat + 4 * g1, M1);
+        FN(mj_body_mat)(quat + 4 * g2, M2);
+        nc = FN(box_box)(pos + 3 * g1, M1, h1, pos + 3 * g2, M2, h2, con);
+    }
+    for (int t = 0; t < nc; ++t) { con[t].partner = (int32_t)j; con[t].self_g1 = g1 == i; }
+    return nc;
+}
+
+/* KAT entry: in[22] = kind1, kind2, c1[3], q1[4], s1[3], c2[3], q2[4], s2[3]
+ * (body 1 has the lower id) -> out[33] = count, then per contact dist,
+ * pos[3], frame[3], kind (from body 1's side: frame as generated). */
+int FN(rbo_kat_narrow)(int64_t n, const double *in, double *out) {
+    for (int64_t c = 0; c < n; ++c) {
+        const double *a = in + 22 * c;
+        int32_t kinds[2] = {(int32_t)a[0], (int32_t)a[1]};
+        double sz[6] = {a[9], a[10], a[11], a[19], a[20], a[21]};
+        rb_scene_desc dd;
+        memset(&dd, 0, sizeof dd);
+        dd.n_bodies = 2;
+        dd.kind = kinds;
+        dd.size = sz;
+        REAL pos[6] = {(REAL)a[2], (REAL)a[3], (REAL)a[4], (REAL)a[12], (REAL)a[13], (REAL)a[14]};
+        REAL quat[8] = {(REAL)a[5], (REAL)a[6], (REAL)a[7], (REAL)a[8], (REAL)a[15], (REAL)a[16], (REAL)a[17], (REAL)a[18]};
+        FN(rbo_contact) con[4];
+        const int nc = FN(pair_contacts)(&dd, pos, quat, 0, 1, con);
+        double *o = out + 33 * c;
+        for (int k = 0; k < 33; ++k) o[k] = 0;
+        o[0] = nc;
+        for (int t = 0; t < nc; ++t) {
+            double *r = o + 1 + 8 * t;
+            r[0] = (double)con[t].dist;
+            for (int k = 0; k < 3; ++k) { r[1 + k] = (double)con[t].pos[k]; r[4 + k] = (double)con[t].frame[k]; }
+            r[7] = con[t].kind;
+        }
+    }
+    return 0;
 }
 
 /* ---------------- broadphase (oracle: exact cell keys, sorted) ------------ */
@@ -363,6 +637,7 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
             }
             for (int t = 0; t < nc; ++t) {
                 tmp[t].partner = -1 - p;
+                tmp[t].self_g1 = 0;
                 cons[off++] = tmp[t];
                 ++cnt;
             }
@@ -384,15 +659,17 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
                         if (j == i) continue;
                         const REAL *cj = pos + 3 * j;
                         if (d->kind[i] != RB_BODY_SPHERE || d->kind[j] != RB_BODY_SPHERE) {
+                            /* box-involved pair: a partner when the bounding spheres overlap
+                             * (the narrowphase may then find no contact) */
                             REAL dd[3] = {ci[0] - cj[0], ci[1] - cj[1], ci[2] - cj[2]};
                             const REAL bi = FN(bound_radius)(d, i), bj = FN(bound_radius)(d, j);
-                            if (SQRT(FN(mj_dot3)(dd, dd)) <= bi + bj) brc = RB_EUNSUPPORTED;
-                            continue;
+                            if (!(SQRT(FN(mj_dot3)(dd, dd)) <= bi + bj)) continue;
+                        } else {
+                            const int64_t g1 = i < j ? i : j, g2 = i < j ? j : i;
+                            FN(rbo_contact) con;
+                            if (!FN(sphere_sphere)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2,
+                                                   (REAL)d->size[3 * g2], &con)) continue;
                         }
-                        const int64_t g1 = i < j ? i : j, g2 = i < j ? j : i;
-                        FN(rbo_contact) con;
-                        if (!FN(sphere_sphere)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2,
-                                               (REAL)d->size[3 * g2], &con)) continue;
                         if (np_ >= maxp) { brc = RB_EOVERFLOW; break; }
                         /* insertion into ascending id order */
                         int s = np_++;
@@ -401,13 +678,9 @@ static int FN(gen_contacts)(const rb_scene_desc *d, const REAL *pos, const REAL 
                     }
                 }
         for (int s = 0; s < np_; ++s) {
-            const int64_t j = plist[s];
-            const int64_t g1 = i < j ? i : j, g2 = i < j ? j : i;
-            FN(rbo_contact) con;
-            FN(sphere_sphere)(pos + 3 * g1, (REAL)d->size[3 * g1], pos + 3 * g2, (REAL)d->size[3 * g2], &con);
-            con.partner = (int32_t)j;
-            cons[off++] = con;
-            ++cnt;
+            FN(rbo_contact) con[4];
+            const int nc = FN(pair_contacts)(d, pos, quat, i, plist[s], con);
+            for (int t = 0; t < nc; ++t) { cons[off++] = con[t]; ++cnt; }
         }
         counts[i] = cnt;
         if (brc) {
@@ -420,6 +693,15 @@ done:
     return rc;
 }
 
+/* contact records per body: 4 per plane, 1 per sphere partner, 4 per
+ * partner in scenes with boxes */
+static int64_t FN(contact_stride)(const rb_scene_desc *d) {
+    const int maxp = d->max_partners > 0 ? d->max_partners : 16;
+    int boxes = 0;
+    for (int64_t i = 0; i < d->n_bodies && !boxes; ++i) boxes = d->kind[i] != RB_BODY_SPHERE;
+    return 4 * (int64_t)d->n_planes + (boxes ? 4 : 1) * (int64_t)maxp;
+}
+
 /* ---------------- the step (a8/a9) ------------------------------------ */
 /* nsteps reference steps on AoS qpos[N*7] / qvel[N*6] (in place).
  * Follows collision.py:56-102 / time_integeration.py:13-72 per body and
@@ -430,9 +712,8 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
                  int32_t *out_counts, int32_t *out_partner, int32_t *out_kind, double *out_dist,
                  int64_t out_cap, int64_t *out_total) {
     const int64_t N = d->n_bodies;
-    const int maxp = d->max_partners > 0 ? d->max_partners : 16;
     const REAL dt = (REAL)dt_, e = (REAL)e_, mu = (REAL)mu_, thr = (REAL)thr_;
-    const int64_t stride = 4 * (int64_t)d->n_planes + maxp;
+    const int64_t stride = FN(contact_stride)(d);
     REAL *pos = (REAL *)calloc(3 * (size_t)(N + 1), sizeof(REAL));
     REAL *quat = (REAL *)calloc(4 * (size_t)(N + 1), sizeof(REAL));
     REAL *vel = (REAL *)malloc(sizeof(REAL) * 6 * (size_t)(N + 1));
@@ -474,8 +755,7 @@ int FN(rbo_step)(const rb_scene_desc *d, double *qpos, double *qvel, const doubl
                 if (!(cc->dist < 0)) continue;                       /* :74 (NaN too) */
                 if (FABS(cc->dist) < thr) continue;                  /* :79-80 */
                 REAL r[3], n[3];
-                const int flip = (d->normal_convention == RB_NORMAL_ORIENTED &&
-                                  cc->kind == RB_CK_SPHERE_SPHERE && i < cc->partner);
+                const int flip = d->normal_convention == RB_NORMAL_ORIENTED && cc->self_g1;
                 for (int k = 0; k < 3; ++k) {
                     r[k] = cc->pos[k] - x[k];                        /* :75 */
                     n[k] = flip ? -cc->frame[k] : cc->frame[k];      /* :76 (D8) */
@@ -526,8 +806,7 @@ int FN(rbo_contacts)(const rb_scene_desc *d, const double *qpos, int32_t *out_co
                      int32_t *out_partner, int32_t *out_kind, double *out_dist, double *out_pos,
                      double *out_frame, int64_t out_cap, int64_t *out_total) {
     const int64_t N = d->n_bodies;
-    const int maxp = d->max_partners > 0 ? d->max_partners : 16;
-    const int64_t stride = 4 * (int64_t)d->n_planes + maxp;
+    const int64_t stride = FN(contact_stride)(d);
     REAL *pos = (REAL *)calloc(3 * (size_t)(N + 1), sizeof(REAL));
     REAL *quat = (REAL *)calloc(4 * (size_t)(N + 1), sizeof(REAL));
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N + 1));

@@ -28,6 +28,9 @@
 
 using namespace rb;
 
+static_assert(CK_SPHERE_BOX == RB_CK_SPHERE_BOX && CK_BOX_BOX0 == RB_CK_BOX_BOX0 && CK_BOX_EDGE == RB_CK_BOX_EDGE,
+              "contact kinds");
+
 namespace {
 
 thread_local std::string g_err;
@@ -61,7 +64,8 @@ int err_to_code(int32_t bits) {
     if (bits & ERR_EXCHANGE) return fail(RB_ENODEV, "device: peer-to-peer exchange timed out (a peer rank did not reach the step)");
     if (bits & ERR_DOMAIN) return fail(RB_EDOM, "device: non-finite or out-of-range body position");
     if (bits & ERR_UNSUPPORTED)
-        return fail(RB_EUNSUPPORTED, "device: box-box / box-sphere pair within contact range (not restated)");
+        return fail(RB_EUNSUPPORTED, "device: box-involved pair within contact range in a sharded world "
+                                     "(box orientations are not exchanged between shards)");
     if (bits & ERR_PARTNER_OVERFLOW) return fail(RB_EOVERFLOW, "device: a body has more sphere partners than max_partners");
     if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: more than 30 bodies hashed to one broadphase bucket");
     return RB_OK;
@@ -85,6 +89,7 @@ struct rb_world {
     double inv_cs = 1.0;
     double rmax = 0.0;             // largest bounding radius
     bool all_spheres = true;
+    bool boxes = false;            // box-capable step kernels (box bodies, unsharded)
     // contact law (rb_set_contact_law)
     int32_t law = RB_LAW_MUJOCO;
     double tol = 0.01;
@@ -93,6 +98,7 @@ struct rb_world {
     int64_t bytes_per_body_step = 0;
     // device memory
     void *snap[2] = {};        // [Npad] Snap<T>: (x, y, z, bound radius), ping-pong
+    void *qsnap[2] = {};       // boxes: [Npad][4] step-start orientations, ping-pong with snap
     void *state = nullptr;     // 13 x S  (qw qx qy qz vx vy vz wx wy wz px py pz)
     void *vel[2] = {};         // two-ball law: [Npad] Vel<T>, ping-pong with the snapshots
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
@@ -196,6 +202,10 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     }
     p.tol = (T)w->tol;
     p.ground = w->n_planes > 0;
+    if (w->boxes) {
+        p.quat_cur = dp<T>(w->qsnap[sp], 0);
+        p.quat_next = dp<T>(w->qsnap[1 - sp], 0);
+    }
     if (w->record) {
         p.rec_count = w->rec_count; p.rec_partner = w->rec_partner; p.rec_kind = w->rec_kind;
         p.rec_dist = dp<T>(w->rec_dist, 0);
@@ -256,8 +266,8 @@ int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, doubl
         return RB_OK;
     }
     const int form = w->n_local <= w->coop_max ? FORM_COOP : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
-    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, form, s);
-    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, form, s);
+    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, form, w->boxes, s);
+    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, form, w->boxes, s);
     HIPCHK(r);
     return RB_OK;
 }
@@ -527,6 +537,13 @@ int upload_state(rb_world *w, const double *qpos, const double *qvel, const doub
     }
     HIPCHK(hipMemcpyAsync(w->snap[w->sp()], sn.data(), sizeof(T) * sn.size(), hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(w->state, st.data(), sizeof(T) * st.size(), hipMemcpyHostToDevice, w->stream));
+    std::vector<T> qs;
+    if (w->boxes) {
+        qs.assign((size_t)4 * w->Npad, T(0));
+        for (int64_t b = 0; b < w->N; ++b)
+            for (int d = 0; d < 4; ++d) qs[(size_t)(4 * b + d)] = (T)qpos[7 * b + 3 + d];
+        HIPCHK(hipMemcpyAsync(w->qsnap[w->sp()], qs.data(), sizeof(T) * qs.size(), hipMemcpyHostToDevice, w->stream));
+    }
     HIPCHK(hipStreamSynchronize(w->stream));
     return RB_OK;
 }
@@ -597,7 +614,7 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *bufs[] = {w->snap[0], w->snap[1], w->state, w->consts, w->kind, w->xfrc, w->gen,
+    void *bufs[] = {w->snap[0], w->snap[1], w->qsnap[0], w->qsnap[1], w->state, w->consts, w->kind, w->xfrc, w->gen,
                     w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
@@ -659,7 +676,14 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     for (int j = 0; j < 3; ++j) w->g[j] = d->gravity[j];
     w->oriented = d->normal_convention == RB_NORMAL_ORIENTED;
     w->maxp = maxp;
-    w->maxrec = 4 * w->n_planes + w->maxp;
+    bool any_box = false;
+    for (int64_t b = 0; b < d->n_bodies && !any_box; ++b) any_box = d->kind[b] != RB_BODY_SPHERE;
+    // box-involved pairs are solved on unsharded worlds (a box partner's
+    // orientation must be the step-start one; shards exchange positions only)
+    w->boxes = any_box && w->P == 1;
+    // records per body: 4 per plane, 1 per sphere partner, up to 4 per
+    // partner in scenes with boxes (oracle/rb_oracle_impl.h contact_stride)
+    w->maxrec = 4 * w->n_planes + (any_box ? 4 : 1) * w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     // per-cell hash, sized so few cells share a bucket and few false
@@ -697,6 +721,8 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
             return bail(fail(RB_ENOMEM, "hipMalloc(%lld) failed", (long long)(bytes)));          \
     } while (0)
     for (int k = 0; k < 2; ++k) ALLOC(w->snap[k], (size_t)w->esz * 4 * w->Npad);
+    if (w->boxes)
+        for (int k = 0; k < 2; ++k) ALLOC(w->qsnap[k], (size_t)w->esz * 4 * w->Npad);
     ALLOC(w->state, (size_t)w->esz * 13 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);
@@ -707,7 +733,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // (DESIGN §5), so the default is the fused one-kernel step.
     const char *split_env = getenv("RBHIP_SPLIT");
     const bool coop = w->n_local <= w->coop_max;
-    const bool split = !coop && split_env && atoi(split_env) == 1;
+    const bool split = !coop && !w->boxes && split_env && atoi(split_env) == 1;
     if (split) {
         ALLOC(w->plist, sizeof(int32_t) * (w->maxp <= 16 ? 16 : 32) * w->S);
         ALLOC(w->plist_cnt, sizeof(int32_t) * w->S);
@@ -1031,6 +1057,7 @@ static int kat_common(int32_t device, int32_t dtype, int64_t n, const double *in
         if (which == 1) e = dtype == RB_F64 ? launch_kat_inertia<double>(n, din, dout, nullptr) : launch_kat_inertia<float>(n, din, dout, nullptr);
         else if (which == 2) e = dtype == RB_F64 ? launch_kat_apply<double>(n, din, dout, nullptr) : launch_kat_apply<float>(n, din, dout, nullptr);
         else if (which == 3) e = dtype == RB_F64 ? launch_kat_pair_impulse<double>(n, din, dout, nullptr) : launch_kat_pair_impulse<float>(n, din, dout, nullptr);
+        else if (which == 4) e = dtype == RB_F64 ? launch_kat_narrow<double>(n, din, dout, nullptr) : launch_kat_narrow<float>(n, din, dout, nullptr);
         else e = dtype == RB_F64 ? launch_kat_impulse<double>(n, din, dout, nullptr) : launch_kat_impulse<float>(n, din, dout, nullptr);
     }
     if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * nout * n, hipMemcpyDeviceToHost);
@@ -1054,6 +1081,10 @@ int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in, dou
 
 int rb_kat_pair_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
     return kat_common(device, dtype, n, in, out, 27, 3, 3);
+}
+
+int rb_kat_narrow(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    return kat_common(device, dtype, n, in, out, 22, 33, 4);
 }
 
 int rb_set_contact_law(rb_world *w, int32_t law, double tol) {

@@ -269,7 +269,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u)
             if (hit(tj[u], sn[u]))
-                list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
+                list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
         base += RB_QBATCH;
         if (base == RB_QBATCH) STAMP(9);
     } while (base < total);
@@ -351,7 +351,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
         }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
-            if (base + u < n && hit(tj[u], sn[u])) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
+            if (base + u < n && hit(tj[u], sn[u])) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
     }
     STAMP(9);
     if (more) {
@@ -372,7 +372,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
                     if (s0 + u < c[k] && hit(tj[u], sn[u]))
-                        list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)tj[u], overflow);
+                        list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
             }
         }
     }

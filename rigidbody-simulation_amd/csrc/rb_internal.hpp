@@ -53,6 +53,11 @@ template <typename T> struct Table {
 
 constexpr int MAX_PLANES = 8;
 
+// contact kinds of box-involved pairs (include/rbhip.h RB_CK_*)
+constexpr int CK_SPHERE_BOX = 17;
+constexpr int CK_BOX_BOX0 = 32;              // + face-clip point index (< 4)
+constexpr int CK_BOX_EDGE = 40;
+
 // Structure-of-arrays body state of this shard.  Positions live in the
 // snapshots, except under the two-ball law, whose snapshots hold the next
 // step's post-ground positions: its true positions are px, py, pz.
@@ -136,6 +141,11 @@ template <typename T> struct StepParams {
     int32_t *rec_count, *rec_partner, *rec_kind;
     T *rec_dist;
     int32_t maxrec;
+    // box-involved pairs (box-capable step kernels only): step-start
+    // orientations w x y z by global id, [Npad][4], ping-pong with the
+    // snapshots (a partner's state row is updated in place during the step)
+    const T *quat_cur;
+    T *quat_next;
 };
 
 static_assert(offsetof(StepParams<double>, xfrc) == 64 && offsetof(StepParams<float>, xfrc) == 64,
@@ -220,13 +230,15 @@ template <typename T> struct HaloParams {
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one
 // lane per body at one wave per SIMD (mid-size scenes)
 enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2 };
-template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, hipStream_t s);
+// boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s);
+template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, double *out, hipStream_t s);
 // two-ball law (rb_balls.hip)
 template <typename T> hipError_t launch_ball_step(const StepParams<T> &p, int maxp, hipStream_t s);
 template <typename T> hipError_t launch_ball_prime(const StepParams<T> &p, hipStream_t s);

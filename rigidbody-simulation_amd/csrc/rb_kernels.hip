@@ -40,6 +40,7 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][16];
 #define STAMP(k) do {} while (0)
 #endif
 
+#include "rb_boxes.hpp"
 #include "rb_grid.hpp"
 #include "rb_internal.hpp"
 
@@ -108,18 +109,23 @@ __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Cont
     if (impulse(m, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
 }
 
-// Candidate test shared by both search forms: true if the candidate with
-// snapshot s and tagged id tj is a sphere partner of body i.
-template <typename T>
+// Candidate test shared by every search form: true if the candidate with
+// snapshot s and tagged id tj is a partner of body i — for two spheres the
+// sphere-sphere contact test, for a box-involved pair overlapping bounding
+// spheres (the narrowphase then decides; oracle gen_contacts does the
+// same).  Kernels without box support (sharded worlds: box orientations
+// are not exchanged) report such a pair as unsupported.
+template <typename T, bool BOXES>
 __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x, T rad, T bi,
                                               uint32_t tj, const Snap<T> &s) {
     const int32_t j = (int32_t)(tj & ~BOX_FLAG);
     if (j == i) return false;
     const V3<T> cj = {s.x, s.y, s.z};
     if (kind != 0 || (tj & BOX_FLAG)) {
-        // box-involved pair: not restated
         const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
-        if (sqroot(mj_dot(dd, dd)) <= bi + s.r) atomicOr(p.err, ERR_UNSUPPORTED);
+        const bool near = sqroot(mj_dot(dd, dd)) <= bi + s.r;
+        if (BOXES) return near;
+        if (near) atomicOr(p.err, ERR_UNSUPPORTED);
         return false;
     }
     return sphere_sphere_hit(x, rad, cj, s.r);
@@ -127,22 +133,23 @@ __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i,
 
 // K1, one lane per body (rb_grid.hpp search_buckets with the main law's
 // candidate test).
-template <typename T, int MAXP>
+template <typename T, int MAXP, bool BOXES>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                    T rad, T bi, int32_t *s_id, int tid, uint32_t gen) {
     return search_buckets<T, MAXP>(p, i, x, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
-        return candidate_hit(p, i, kind, x, rad, bi, tj, s);
+        return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s);
     });
 }
 
 // K1, wide one-lane form (rb_grid.hpp search_buckets_wide)
-template <typename T, int MAXP, typename Overlap>
+template <typename T, int MAXP, bool BOXES, typename Overlap>
 __device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                         T rad, T bi, int32_t *s_id, uint32_t *s_cand, int tid,
                                                         uint32_t gen, Overlap overlap) {
     return search_buckets_wide<T, MAXP>(
         p, i, x, s_id, s_cand, tid, gen,
-        [&](uint32_t tj, const Snap<T> &s) { return candidate_hit(p, i, kind, x, rad, bi, tj, s); }, overlap);
+        [&](uint32_t tj, const Snap<T> &s) { return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s); },
+        overlap);
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
@@ -153,7 +160,7 @@ __device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, 
 // (shuffles) places them — id and snapshot — in LDS, and the group
 // rank-sorts them by body id into s_id / s_pos.  Same contact set and order
 // as search_partners.
-template <typename T, int MAXP, int G, typename Overlap>
+template <typename T, int MAXP, int G, bool BOXES, typename Overlap>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
                                                V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
                                                Snap<T> *t_pos, int slot, int k, int lane, uint32_t gen,
@@ -192,7 +199,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     uint32_t mask = 0;
 #pragma unroll
     for (int u = 0; u < QS; ++u)
-        if (u < c && candidate_hit(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u])) mask |= 1u << u;
+        if (u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u])) mask |= 1u << u;
     for (int s0 = QS; s0 < c; s0 += QB) {
         uint32_t tj[QB];
         Snap<T> sn[QB];
@@ -204,7 +211,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
-            if (s0 + u < c && candidate_hit(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
+            if (s0 + u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
     }
     STAMP(10);
     const int h = __popc(mask);
@@ -221,7 +228,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     for (int u = 0; u < QS; ++u) {
         if (!((mask >> u) & 1u)) continue;
         if (o < MAXP) {
-            t_id[slot * MAXP + o] = (int32_t)bucket_id(p.cur, b, id4, u);
+            t_id[slot * MAXP + o] = (int32_t)(bucket_id(p.cur, b, id4, u) & ~BOX_FLAG);
             t_pos[slot * MAXP + o] = p4[u];
         }
         ++o;
@@ -229,7 +236,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     for (uint32_t rest = mask & ~((1u << QS) - 1u); rest; rest &= rest - 1) {
         const int sl = __builtin_ctz(rest);
         if (o < MAXP) {                               // re-read: L1-hot from the batch above
-            t_id[slot * MAXP + o] = (int32_t)bucket_id(p.cur, b, id4, sl);
+            t_id[slot * MAXP + o] = (int32_t)(bucket_id(p.cur, b, id4, sl) & ~BOX_FLAG);
             t_pos[slot * MAXP + o] = p.cur.pos[base + sl];
         }
         ++o;
@@ -288,11 +295,12 @@ __device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T
 // split form's per-slot list in HBM); snapshots at ppos[u * stride] (LDS,
 // POS = true: cooperative form) or gathered from the step-start snapshot.
 // POS is a template flag so LDS accesses stay ds_read (no flat loads).
-template <typename T, bool POS>
+template <typename T, bool POS, bool BOXES = false>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, bool forced, LazyInvI<T> &invI,
                                             int32_t np_, const int32_t *pid, int64_t stride, const Snap<T> *ppos,
-                                            int tid, int32_t *cell, uint32_t gen_next) {
+                                            int tid, int32_t *cell, uint32_t gen_next, T *poly = nullptr,
+                                            int ps = 0) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -313,8 +321,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             record(p, l, nrec, -1 - pl, 0, con.dist);
             solve_contact(p, con, x, con.frame, m, invI, v, w);
         }
-    } else {
-        const M3<T> M = mj_body_mat(q);
+    }
+    M3<T> M;                                       // box orientation (mj_kinematics of the free joint)
+    if (kind != 0) M = mj_body_mat(q);
+    if (kind != 0) {
         for (int pl = 0; pl < p.n_planes; ++pl) {
             const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
             const V3<T> dif = {x.x - p.pp[pl][0], x.y - p.pp[pl][1], x.z - p.pp[pl][2]};
@@ -351,6 +361,41 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             const int32_t j = jj[u];
             const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};
             const T rj = pe[u].r;
+            if constexpr (BOXES) {
+                const int32_t kj = p.cs.kind[j];
+                if (kind != 0 || kj != 0) {
+                    // box-involved pair (rb_boxes.hpp), from step-start data of both
+                    // bodies, in MuJoCo's geom order: sphere before box, boxes by id
+                    auto emit = [&](const Contact<T> &con, int ck, bool self_g1) {
+                        record(p, l, nrec, j, ck, con.dist);
+                        const V3<T> n = (p.oriented && self_g1) ? V3<T>{-con.frame.x, -con.frame.y, -con.frame.z}
+                                                                : con.frame;
+                        solve_contact(p, con, x, n, m, invI, v, w);
+                    };
+                    M3<T> Mj;
+                    const V3<T> hj = {p.cs.sx()[j], p.cs.sy()[j], p.cs.sz()[j]};
+                    if (kj != 0) {
+                        const T *qj = p.quat_cur + 4 * (int64_t)j;
+                        Mj = mj_body_mat(Q4<T>{qj[0], qj[1], qj[2], qj[3]});
+                    }
+                    // geom1: the sphere of a sphere-box pair, else the lower id
+                    // (one call of each primitive, operands selected)
+                    const bool g1 = (kind == 0 && kj != 0) || (kind != 0 && kj != 0 && i < j);
+                    const V3<T> p1 = g1 ? x : cj, p2 = g1 ? cj : x;
+                    const V3<T> h1 = g1 ? sz : hj, h2 = g1 ? hj : sz;
+                    M3<T> M1, M2;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) { M1.a[k] = g1 ? M.a[k] : Mj.a[k]; M2.a[k] = g1 ? Mj.a[k] : M.a[k]; }
+                    if (kind == 0 || kj == 0) {
+                        Contact<T> con;
+                        if (sphere_box(p1, g1 ? sz.x : rj, p2, M2, h2, con)) emit(con, CK_SPHERE_BOX, g1);
+                    } else {
+                        box_box(p1, M1, h1, p2, M2, h2, poly, ps,
+                                [&](const Contact<T> &c, int ck) { emit(c, ck, g1); });
+                    }
+                    continue;
+                }
+            }
             Contact<T> con;
             V3<T> n;
             if (i < j) {                        // this body is geom1
@@ -391,6 +436,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     wt_store(p.st.wx() + l, w.x); wt_store(p.st.wy() + l, w.y); wt_store(p.st.wz() + l, w.z);
     wt_store(p.st.qw() + l, qn.w); wt_store(p.st.qx() + l, qn.x); wt_store(p.st.qy() + l, qn.y);
     wt_store(p.st.qz() + l, qn.z);
+    if (BOXES && kind != 0) {                   // next step's orientation snapshot
+        T *qs = p.quat_next + 4 * (int64_t)i;
+        wt_store(qs + 0, qn.w); wt_store(qs + 1, qn.x); wt_store(qs + 2, qn.y); wt_store(qs + 3, qn.z);
+    }
     publish_slot(p.next, p.err, cl, sn, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
     STAMP(6);
 }
@@ -398,10 +447,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 // One body (G lanes): contact search, then (lane 0) the update.  WIDE: the
 // one-lane form for one wave per SIMD (search_buckets_wide; state loads and
 // inv(I_w) under the head loads).
-template <typename T, int MAXP, int G, bool WIDE>
+template <typename T, int MAXP, int G, bool WIDE, bool BOXES>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
-                                          uint32_t *s_cand, int32_t *cell, uint32_t gen) {
+                                          uint32_t *s_cand, int32_t *cell, uint32_t gen, T *s_poly) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = p.lo + l;
@@ -428,7 +477,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     int32_t np_ = 0;
     if constexpr (G == 1 && WIDE) {
         if (RB_ABLATE != 1)
-            np_ = search_partners_wide<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, s_cand, tid, gen, [&] {
+            np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, tid, gen, [&] {
                 invI.get();
                 if (!p.xfrc) {
                     apply_force(p, l, in.m, invI, in.v, in.w);
@@ -436,10 +485,10 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
                 }
             });
     } else if constexpr (G == 1) {
-        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP>(p, i, kind, x, sz.x, bi, s_id, tid, gen);
+        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, tid, gen);
     } else {
         if (RB_ABLATE != 1)
-            np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
+            np_ = search_coop<T, MAXP, G, BOXES>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
                                           gen, [&] {
                                               invI.get();
                                               if (!p.xfrc) {
@@ -456,8 +505,8 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
         invI.I = in.I;
         invI.q = in.q;
     }
-    body_update<T, (G > 1)>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB, s_pos + slot, tid,
-                            cell, gen + 1u);
+    body_update<T, (G > 1), BOXES>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB, s_pos + slot,
+                                   tid, cell, gen + 1u, BOXES ? s_poly + slot : nullptr, NB);
 }
 
 // Halo exchange: fold the wave's new cells (cell[0] == INT32_MAX: none) into
@@ -485,10 +534,11 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
     }
 }
 
-template <typename T, int MAXP, int G, bool WIDE = false>
+template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false>
 __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
+    __shared__ T s_poly[BOXES ? 48 * NB : 1];   // box-box face clipping: 2 x 8 vertices x 3 per body
     __shared__ uint32_t s_cand[WIDE ? WIDE_MAXC * NB : 1];
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
@@ -518,7 +568,8 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     const bool active = lb < p.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
     if (G > 1 || active)
-        body_step<T, MAXP, G, WIDE>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen);
+        body_step<T, MAXP, G, WIDE, BOXES>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen,
+                                           s_poly);
     if (p.bounds) fold_bounds(p.bounds, cell);
     if (late_publish && blockIdx.x == 0 && tid == 0) {
         if (p.next.line) *p.next.gen = gen + 1u;
@@ -540,17 +591,25 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(MAXP <= 16 ? RB_MIN_WAVES_COOP : 2)))   // 32 partners: 2 fit
-void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8>(p); }
+void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8, false, false>(p); }
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
 #if RB_MIN_WAVES_G1 > 1
 __attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_G1)))
 #endif
-void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1>(p); }
+void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1, false, false>(p); }
+// box-capable forms (box-box / sphere-box narrowphase): one wave per SIMD,
+// so the narrowphase's registers fit without scratch
+template <typename T, int MAXP>
+__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void step_kernel_coop_box(StepParams<T> p) { step_body<T, MAXP, 8, false, true>(p); }
+template <typename T, int MAXP>
+__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void step_kernel_one_box(StepParams<T> p) { step_body<T, MAXP, 1, false, true>(p); }
 // one wave per SIMD (up to 64 x 1024 owned bodies): every register is free
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void step_kernel_wide(StepParams<T> p) { step_body<T, MAXP, 1, true>(p); }
+void step_kernel_wide(StepParams<T> p) { step_body<T, MAXP, 1, true, false>(p); }
 
 // ---- split form (large scenes): search kernel + update kernel -------------
 // The fused kernel's register footprint (the f64 solve) caps it at two
@@ -578,8 +637,8 @@ __global__ __launch_bounds__(STEP_BLOCK) void search_kernel(StepParams<T> p) {
     const T rad = p.cs.sx()[i];
     const uint32_t gen = *p.cur.gen;
     int32_t np_;
-    if constexpr (G == 1) np_ = search_partners<T, MAXP>(p, i, kind, x, rad, self.r, s_id, tid, gen);
-    else np_ = search_coop<T, MAXP, G>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
+    if constexpr (G == 1) np_ = search_partners<T, MAXP, false>(p, i, kind, x, rad, self.r, s_id, tid, gen);
+    else np_ = search_coop<T, MAXP, G, false>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
                                        gen, [] {});
     if (!active) return;
     for (int s = k; s < np_; s += G) p.plist[CHK((int64_t)s * p.S + l, (int64_t)MAXP * p.S)] = s_id[s * NB + slot];
@@ -612,7 +671,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
     if (p.bounds) fold_bounds(p.bounds, cell);
 }
 
-#if RB_STAMPS
+#if RB_STAMPS && (!defined(RB_INST) || (RB_INST & 1))
 extern "C" int rb_diag_stamps(unsigned long long *out, int nblocks) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 16 * nblocks);
 }
@@ -666,13 +725,50 @@ __global__ void kat_apply_kernel(int64_t n, const double *in, double *out) {
     o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = w.x; o[4] = w.y; o[5] = w.z;
 }
 
+// in[22] = kind1, kind2, c1[3], q1[4], s1[3], c2[3], q2[4], s2[3] (body 1 =
+// lower id) -> out[33] = count, then per contact dist, pos[3], frame[3], kind
+template <typename T>
+__global__ __launch_bounds__(64) void kat_narrow_kernel(int64_t n, const double *in, double *out) {
+    __shared__ T s_poly[48 * 64];
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const double *a = in + 22 * c;
+    double *o = out + 33 * c;
+    for (int k = 0; k < 33; ++k) o[k] = 0;
+    const int k1 = (int)a[0], k2 = (int)a[1];
+    const V3<T> c1 = {(T)a[2], (T)a[3], (T)a[4]}, c2 = {(T)a[12], (T)a[13], (T)a[14]};
+    const Q4<T> q1 = {(T)a[5], (T)a[6], (T)a[7], (T)a[8]}, q2 = {(T)a[15], (T)a[16], (T)a[17], (T)a[18]};
+    const V3<T> s1 = {(T)a[9], (T)a[10], (T)a[11]}, s2 = {(T)a[19], (T)a[20], (T)a[21]};
+    int m = 0;
+    auto emit = [&](const Contact<T> &con, int ck) {
+        double *r = o + 1 + 8 * m;
+        r[0] = (double)con.dist;
+        r[1] = (double)con.pos.x; r[2] = (double)con.pos.y; r[3] = (double)con.pos.z;
+        r[4] = (double)con.frame.x; r[5] = (double)con.frame.y; r[6] = (double)con.frame.z;
+        r[7] = ck;
+        ++m;
+    };
+    Contact<T> con;
+    if (k1 == 0 && k2 == 0) {
+        if (sphere_sphere(c1, s1.x, c2, s2.x, con)) emit(con, 16);
+    } else if (k1 == 0) {
+        if (sphere_box(c1, s1.x, c2, mj_body_mat(q2), s2, con)) emit(con, CK_SPHERE_BOX);
+    } else if (k2 == 0) {
+        if (sphere_box(c2, s2.x, c1, mj_body_mat(q1), s1, con)) emit(con, CK_SPHERE_BOX);
+    } else {
+        box_box(c1, mj_body_mat(q1), s1, c2, mj_body_mat(q2), s2, s_poly + threadIdx.x, 64, emit);
+    }
+    o[0] = m;
+}
+
 // ---- launchers ----------------------------------------------------------
-template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, hipStream_t s) {
+template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s) {
     const bool coop = form == FORM_COOP;
     const int nb = coop ? STEP_BLOCK / 8 : STEP_BLOCK;
     int64_t blocks = (p.n_local + nb - 1) / nb;
     if (blocks < 1) blocks = 1;
-    const bool split = !coop && p.plist;
+    const bool split = !coop && p.plist && !boxes;
+    if (boxes && !p.quat_cur) return hipErrorInvalidValue;
     // the cooperative search reads bucket slot snapshots: never launch it
     // on a table without them
     if (needs_slot_snapshots(coop, split) && (!p.cur.pos || (p.next.line && !p.next.pos))) return hipErrorInvalidValue;
@@ -682,6 +778,15 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
         if (maxp <= 16) hipLaunchKernelGGL((search_kernel<T, 16, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    } else if (boxes) {
+        // box-capable forms (box scenes are small): cooperative or one-lane
+        if (coop) {
+            if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop_box<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+            else hipLaunchKernelGGL((step_kernel_coop_box<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        } else {
+            if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one_box<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+            else hipLaunchKernelGGL((step_kernel_one_box<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        }
     } else if (coop) {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
@@ -720,15 +825,32 @@ template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, d
     return hipGetLastError();
 }
 
-template hipError_t launch_step<double>(const StepParams<double> &, int, int, hipStream_t);
-template hipError_t launch_step<float>(const StepParams<float> &, int, int, hipStream_t);
+template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, double *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL((kat_narrow_kernel<T>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, n, in, out);
+    return hipGetLastError();
+}
+
+// explicit instantiations: RB_INST bit 1 = fp64, bit 2 = fp32 (the Makefile
+// builds the two halves as separate objects, in parallel)
+#ifndef RB_INST
+#define RB_INST 3
+#endif
+#if RB_INST & 1
+template hipError_t launch_step<double>(const StepParams<double> &, int, int, bool, hipStream_t);
+template hipError_t launch_kat_narrow<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
-template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
 template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *, hipStream_t);
-template hipError_t launch_kat_impulse<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<double>(int64_t, const double *, double *, hipStream_t);
-template hipError_t launch_kat_inertia<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
+#endif
+#if RB_INST & 2
+template hipError_t launch_step<float>(const StepParams<float> &, int, int, bool, hipStream_t);
+template hipError_t launch_kat_narrow<float>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
+template hipError_t launch_kat_impulse<float>(int64_t, const double *, double *, hipStream_t);
+template hipError_t launch_kat_inertia<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);
+#endif
 
 }  // namespace rb

@@ -11,6 +11,7 @@ way the reference puts its repo root on PYTHONPATH for `src.*`).
 """
 from . import scenes  # noqa: F401
 from ._lib import RbError, load  # noqa: F401
-from .world import World, kat_apply, kat_impulse, kat_inertia, kat_pair_impulse  # noqa: F401
+from .world import World, kat_apply, kat_impulse, kat_inertia, kat_narrow, kat_pair_impulse  # noqa: F401
 
-__all__ = ["World", "RbError", "load", "scenes", "kat_impulse", "kat_inertia", "kat_apply", "kat_pair_impulse"]
+__all__ = ["World", "RbError", "load", "scenes", "kat_impulse", "kat_inertia", "kat_apply", "kat_pair_impulse",
+           "kat_narrow"]

@@ -20,6 +20,7 @@ RB_BODY_SPHERE, RB_BODY_BOX = 0, 1
 RB_F64, RB_F32 = 0, 1
 RB_NORMAL_ORIENTED, RB_NORMAL_RAW = 0, 1
 RB_CK_PLANE_SPHERE, RB_CK_PLANE_BOX0, RB_CK_SPHERE_SPHERE = 0, 1, 16
+RB_CK_SPHERE_BOX, RB_CK_BOX_BOX0, RB_CK_BOX_EDGE = 17, 32, 40
 RB_LAW_MUJOCO, RB_LAW_BALLS = 0, 1
 
 
@@ -67,6 +68,7 @@ SIGNATURES = {
     "rb_kat_inertia": (C.c_int, [_I32, _I32, _I64, _P, _P]),
     "rb_kat_apply": (C.c_int, [_I32, _I32, _I64, _P, _P]),
     "rb_kat_pair_impulse": (C.c_int, [_I32, _I32, _I64, _P, _P]),
+    "rb_kat_narrow": (C.c_int, [_I32, _I32, _I64, _P, _P]),
     "rb_set_contact_law": (C.c_int, [_P, _I32, _D]),
     "rb_query": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     "rb_kernel_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(_I64)]),

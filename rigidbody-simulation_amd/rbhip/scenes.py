@@ -215,6 +215,46 @@ def incline_cubes(nx: int, ny: int, seed: int = 0, spacing: float = 3.0) -> Scen
                  np.zeros((n, 6)), dt=0.009, restitution=0.2, friction=0.6, threshold=1e-4)
 
 
+def box_pile(nx: int, ny: int, layers: int = 3, seed: int = 0, spacing: float = 1.1, h: float = 0.4,
+             sphere_every: int = 3) -> Scene:
+    """Box-involved contacts (stacking, the Guendelman
+    scheme's goal, README.md:18-24): columns of `layers` cubes of
+    models/cube.xml's size (half extent 0.4, m 25.6, I 2.7307; other h:
+    density 50) on an nx*ny grid with spacing 1.1 (few bounding-sphere
+    partners per box at rest), stacked with 0.03 gaps and tilted by up to
+    0.2 rad about a random axis, so they land on each other (face-face), lean
+    into their neighbours (edge-edge) and topple; every `sphere_every`-th
+    column is capped with a sphere r 0.1 (sphere-box).  Flat ground, e 0.2,
+    mu 0.6 (sim_overrides.py:9-15), dt 0.005.  Use max_partners=32."""
+    rng = np.random.default_rng(seed)
+    m_box = M_CUBE_H04 if h == 0.4 else 50.0 * (2 * h) ** 3
+    i_box = I_CUBE_H04 if h == 0.4 else m_box * (2 * h) ** 2 / 6.0
+    kind, mass, inertia, size, qpos = [], [], [], [], []
+    col = 0
+    for iy in range(ny):
+        for ix in range(nx):
+            x = (ix - (nx - 1) / 2.0) * spacing
+            y = (iy - (ny - 1) / 2.0) * spacing
+            for k in range(layers):
+                ax = rng.normal(size=3)
+                ax /= np.linalg.norm(ax)
+                ang = rng.uniform(0.0, 0.2)
+                q = np.concatenate([[np.cos(ang / 2)], np.sin(ang / 2) * ax])
+                z = h + k * (2 * h + 0.03) + rng.uniform(0.0, 0.02)
+                kind.append(BOX); mass.append(m_box); inertia.append([i_box] * 3); size.append([h, h, h])
+                qpos.append([x + rng.uniform(-0.03, 0.03), y + rng.uniform(-0.03, 0.03), z, *q])
+            if sphere_every and col % sphere_every == 0:
+                z = h + layers * (2 * h + 0.03) + 0.12
+                kind.append(SPHERE); mass.append(M_SPHERE_R01); inertia.append([I_SPHERE_R01] * 3)
+                size.append([0.1, 0.0, 0.0]); qpos.append([x + rng.uniform(-0.1, 0.1), y, z, 1.0, 0, 0, 0])
+            col += 1
+    n = len(kind)
+    qvel = np.zeros((n, 6))
+    qvel[:, 3:6] = rng.normal(0.0, 0.5, (n, 3))
+    return Scene(f"box_pile_{n}", np.array(kind, np.int32), np.array(mass), np.array(inertia), np.array(size),
+                 _flat_plane(), np.array(qpos), qvel, dt=0.005, restitution=0.2, friction=0.6, threshold=0.0)
+
+
 CONFIGS = {
     # BASELINE.json configs, in order
     "c1": single_sphere,

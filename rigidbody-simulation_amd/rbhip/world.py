@@ -51,7 +51,9 @@ class World:
         _lib.check(L.rb_world_create(C.byref(h), C.byref(d)), "rb_world_create")
         self._h = h
         self._L = L
-        self.maxrec = 4 * d.n_planes + max_partners
+        # records per body (rb_world_create): 4 per plane, 1 per sphere
+        # partner, up to 4 per partner in scenes with boxes
+        self.maxrec = 4 * d.n_planes + (4 if bool(np.any(self._kind != 0)) else 1) * max_partners
         n_owned, bpb = C.c_int64(), C.c_int64()
         _lib.check(L.rb_query(h, C.byref(n_owned), C.byref(bpb)), "rb_query")
         self.n_owned = n_owned.value
@@ -250,4 +252,16 @@ def kat_pair_impulse(inp: np.ndarray, dtype: str = "f64", device: int = 0) -> np
     out = np.zeros((inp.shape[0], 3))
     _lib.check(L.rb_kat_pair_impulse(device, _lib.RB_F64 if dtype == "f64" else _lib.RB_F32, inp.shape[0],
                                      _lib.ptr(inp), _lib.ptr(out)), "rb_kat_pair_impulse")
+    return out
+
+
+def kat_narrow(inp: np.ndarray, dtype: str = "f64", device: int = 0) -> np.ndarray:
+    """Device entry for the box-involved narrowphase (rb_boxes.hpp; SURVEY
+    §8f row 4) per row of inp[:, 22] = kind1, kind2, c1, q1, s1, c2, q2, s2
+    -> out[:, 33] = count, then per contact dist, pos[3], frame[3], kind."""
+    L = _lib.load()
+    inp = np.ascontiguousarray(inp, np.float64).reshape(-1, 22)
+    out = np.zeros((inp.shape[0], 33))
+    _lib.check(L.rb_kat_narrow(device, _lib.RB_F64 if dtype == "f64" else _lib.RB_F32, inp.shape[0],
+                               _lib.ptr(inp), _lib.ptr(out)), "rb_kat_narrow")
     return out

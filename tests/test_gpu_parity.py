@@ -332,12 +332,16 @@ def test_nonfinite_position_is_an_error(rb):
             w.step(1)
 
 
-def test_box_pair_is_unsupported(rb):
+def test_box_pair_across_shards_is_unsupported(rb):
+    """Box-involved pairs are solved in unsharded worlds (tests/test_gpu_boxes.py);
+    a sharded world exchanges positions only, so one within contact range is
+    reported instead of being solved with a stale partner orientation."""
     from rbhip import scenes
     sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)
-    with rb.World(sc) as w:
+    with rb.World(sc, rank=0, world_size=2) as w:
         with pytest.raises(rb.RbError, match="EUNSUPPORTED"):
-            w.step(1)
+            w.shard_step()
+            w.sync()
 
 
 def test_kernel_timing_reports_launches(rb):

@@ -101,11 +101,20 @@ def test_oracle_f32_close_to_f64(oracle):
     assert np.abs(q64 - q32).max() < 1e-3
 
 
-def test_oracle_rejects_box_pairs(oracle):
+def test_oracle_overlapping_cubes_get_box_contacts(oracle):
+    """Two cubes 0.5 apart on the incline (they overlap): box-box contacts
+    (rb_oracle_impl.h box_box) in both bodies' lists, the
+    same records from either side, normals opposite under ORIENTED."""
     from rbhip import scenes
-    sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)    # cubes overlapping
-    with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
-        oracle.step(oracle.OracleScene(sc), sc.qpos0, sc.qvel0, 1)
+    sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)
+    osc = oracle.OracleScene(sc)
+    cnt, par, kin, dis, pos, frm = oracle.contacts(osc, sc.qpos0)
+    bb = kin >= 32
+    assert bb.sum() >= 2 and set(par[bb].tolist()) == {0, 1}
+    a, b = (par == 1) & bb, (par == 0) & bb
+    assert np.array_equal(dis[a], dis[b]) and np.array_equal(pos[a], pos[b]) and np.array_equal(frm[a], frm[b])
+    q, v = oracle.step(osc, sc.qpos0, sc.qvel0, 5)
+    assert np.isfinite(q).all()
 
 
 def test_oracle_thread_count_invariant(oracle):
