@@ -99,6 +99,8 @@ struct rb_world {
     // device memory
     void *snap[2] = {};        // [Npad] Snap<T>: (x, y, z, bound radius), ping-pong
     void *qsnap[2] = {};       // boxes: [Npad][4] step-start orientations, ping-pong with snap
+    int32_t *defer_q = nullptr;    // boxes: [S] bodies the step kernel defers to the box kernel
+    int32_t *defer_cnt = nullptr;  // boxes: [2] queue lengths by step parity
     void *state = nullptr;     // 13 x S  (qw qx qy qz vx vy vz wx wy wz px py pz)
     void *vel[2] = {};         // two-ball law: [Npad] Vel<T>, ping-pong with the snapshots
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
@@ -205,6 +207,9 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     if (w->boxes) {
         p.quat_cur = dp<T>(w->qsnap[sp], 0);
         p.quat_next = dp<T>(w->qsnap[1 - sp], 0);
+        p.defer_q = w->defer_q;
+        p.defer_cnt = w->defer_cnt + sp;
+        p.defer_reset = w->defer_cnt + (1 - sp);
     }
     if (w->record) {
         p.rec_count = w->rec_count; p.rec_partner = w->rec_partner; p.rec_kind = w->rec_kind;
@@ -614,7 +619,7 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *bufs[] = {w->snap[0], w->snap[1], w->qsnap[0], w->qsnap[1], w->state, w->consts, w->kind, w->xfrc, w->gen,
+    void *bufs[] = {w->snap[0], w->snap[1], w->qsnap[0], w->qsnap[1], w->defer_q, w->defer_cnt, w->state, w->consts, w->kind, w->xfrc, w->gen,
                     w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
@@ -721,8 +726,12 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
             return bail(fail(RB_ENOMEM, "hipMalloc(%lld) failed", (long long)(bytes)));          \
     } while (0)
     for (int k = 0; k < 2; ++k) ALLOC(w->snap[k], (size_t)w->esz * 4 * w->Npad);
-    if (w->boxes)
+    if (w->boxes) {
         for (int k = 0; k < 2; ++k) ALLOC(w->qsnap[k], (size_t)w->esz * 4 * w->Npad);
+        ALLOC(w->defer_q, sizeof(int32_t) * (w->S > 0 ? w->S : 1));
+        ALLOC(w->defer_cnt, sizeof(int32_t) * 2);
+        if (hipMemset(w->defer_cnt, 0, sizeof(int32_t) * 2) != hipSuccess) return bail(fail(RB_ENODEV, "hipMemset failed"));
+    }
     ALLOC(w->state, (size_t)w->esz * 13 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
     ALLOC(w->kind, sizeof(int32_t) * w->Npad);

@@ -146,6 +146,12 @@ template <typename T> struct StepParams {
     // snapshots (a partner's state row is updated in place during the step)
     const T *quat_cur;
     T *quat_next;
+    // box worlds: the step kernel defers a body with a box-involved partner
+    // within bounding range to the box kernel (queue of local indices,
+    // counter of this step parity; the box kernel zeroes the other parity's)
+    int32_t *defer_q;
+    int32_t *defer_cnt;
+    int32_t *defer_reset;
 };
 
 static_assert(offsetof(StepParams<double>, xfrc) == 64 && offsetof(StepParams<float>, xfrc) == 64,

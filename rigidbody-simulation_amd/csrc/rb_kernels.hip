@@ -113,11 +113,12 @@ __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Cont
 // snapshot s and tagged id tj is a partner of body i — for two spheres the
 // sphere-sphere contact test, for a box-involved pair overlapping bounding
 // spheres (the narrowphase then decides; oracle gen_contacts does the
-// same).  Kernels without box support (sharded worlds: box orientations
-// are not exchanged) report such a pair as unsupported.
+// same).  Only the box kernel (BOXES) takes such a pair; the sphere step
+// kernels mark the body deferred to it (box worlds: p.defer_q) or, in
+// sharded worlds (box orientations are not exchanged), report it.
 template <typename T, bool BOXES>
 __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x, T rad, T bi,
-                                              uint32_t tj, const Snap<T> &s) {
+                                              uint32_t tj, const Snap<T> &s, bool &defer) {
     const int32_t j = (int32_t)(tj & ~BOX_FLAG);
     if (j == i) return false;
     const V3<T> cj = {s.x, s.y, s.z};
@@ -125,7 +126,10 @@ __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i,
         const V3<T> dd = {x.x - cj.x, x.y - cj.y, x.z - cj.z};
         const bool near = sqroot(mj_dot(dd, dd)) <= bi + s.r;
         if (BOXES) return near;
-        if (near) atomicOr(p.err, ERR_UNSUPPORTED);
+        if (near) {
+            if (p.defer_q) defer = true;
+            else atomicOr(p.err, ERR_UNSUPPORTED);
+        }
         return false;
     }
     return sphere_sphere_hit(x, rad, cj, s.r);
@@ -135,9 +139,9 @@ __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i,
 // candidate test).
 template <typename T, int MAXP, bool BOXES>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
-                                                   T rad, T bi, int32_t *s_id, int tid, uint32_t gen) {
+                                                   T rad, T bi, int32_t *s_id, int tid, uint32_t gen, bool &defer) {
     return search_buckets<T, MAXP>(p, i, x, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
-        return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s);
+        return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s, defer);
     });
 }
 
@@ -145,10 +149,10 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
 template <typename T, int MAXP, bool BOXES, typename Overlap>
 __device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                         T rad, T bi, int32_t *s_id, uint32_t *s_cand, int tid,
-                                                        uint32_t gen, Overlap overlap) {
+                                                        uint32_t gen, bool &defer, Overlap overlap) {
     return search_buckets_wide<T, MAXP>(
         p, i, x, s_id, s_cand, tid, gen,
-        [&](uint32_t tj, const Snap<T> &s) { return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s); },
+        [&](uint32_t tj, const Snap<T> &s) { return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s, defer); },
         overlap);
 }
 
@@ -164,7 +168,7 @@ template <typename T, int MAXP, int G, bool BOXES, typename Overlap>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
                                                V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
                                                Snap<T> *t_pos, int slot, int k, int lane, uint32_t gen,
-                                               Overlap overlap) {
+                                               bool &defer, Overlap overlap) {
     static_assert(G == 8, "one lane per neighbour cell");
     constexpr int NB = STEP_BLOCK / G;
     constexpr int QB = RB_QBATCH;
@@ -199,7 +203,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     uint32_t mask = 0;
 #pragma unroll
     for (int u = 0; u < QS; ++u)
-        if (u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u])) mask |= 1u << u;
+        if (u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u], defer)) mask |= 1u << u;
     for (int s0 = QS; s0 < c; s0 += QB) {
         uint32_t tj[QB];
         Snap<T> sn[QB];
@@ -211,9 +215,16 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
-            if (s0 + u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj[u], sn[u])) mask |= 1u << (s0 + u);
+            if (s0 + u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj[u], sn[u], defer)) mask |= 1u << (s0 + u);
     }
     STAMP(10);
+    if (p.defer_q) {                              // any lane of the group: the body is deferred
+        int dv = defer ? 1 : 0;
+        dv |= __shfl_xor(dv, 1);
+        dv |= __shfl_xor(dv, 2);
+        dv |= __shfl_xor(dv, 4);
+        defer = dv != 0;
+    }
     const int h = __popc(mask);
     int pre_n = 0, total = 0;
 #pragma unroll
@@ -475,9 +486,10 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     }
     STAMP(1);
     int32_t np_ = 0;
+    bool defer = false;                          // a box-involved partner in range: the box kernel steps it
     if constexpr (G == 1 && WIDE) {
         if (RB_ABLATE != 1)
-            np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, tid, gen, [&] {
+            np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, tid, gen, defer, [&] {
                 invI.get();
                 if (!p.xfrc) {
                     apply_force(p, l, in.m, invI, in.v, in.w);
@@ -485,11 +497,11 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
                 }
             });
     } else if constexpr (G == 1) {
-        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, tid, gen);
+        if (RB_ABLATE != 1) np_ = search_partners<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, tid, gen, defer);
     } else {
         if (RB_ABLATE != 1)
             np_ = search_coop<T, MAXP, G, BOXES>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                          gen, [&] {
+                                          gen, defer, [&] {
                                               invI.get();
                                               if (!p.xfrc) {
                                                   apply_force(p, l, in.m, invI, in.v, in.w);
@@ -500,6 +512,10 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     STAMP(2);
     if (RB_ABLATE == 7) np_ = 0;                 // diagnostic: search, but solve no partner contact
     if (!active || k != 0 || RB_ABLATE == 4) return;
+    if (!BOXES && defer) {                       // box worlds only (p.defer_q set)
+        p.defer_q[atomicAdd(p.defer_cnt, 1)] = l;
+        return;
+    }
     if constexpr (!early) {
         in = load_body(p, l, i);
         invI.I = in.I;
@@ -598,14 +614,27 @@ __global__ __launch_bounds__(STEP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_G1)))
 #endif
 void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1, false, false>(p); }
-// box-capable forms (box-box / sphere-box narrowphase): one wave per SIMD,
-// so the narrowphase's registers fit without scratch
+// The box kernel (box worlds, after the step kernel): steps the bodies the
+// step kernel deferred — those with a box-involved partner within bounding
+// range — one lane per body with the box narrowphase (rb_boxes.hpp), from
+// the same step-start data, so the step stays Jacobi across bodies.  One
+// wave per SIMD: the narrowphase's registers fit without scratch, and the
+// sphere step kernels keep their occupancy.
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void step_kernel_coop_box(StepParams<T> p) { step_body<T, MAXP, 8, false, true>(p); }
-template <typename T, int MAXP>
-__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void step_kernel_one_box(StepParams<T> p) { step_body<T, MAXP, 1, false, true>(p); }
+void box_kernel(StepParams<T> p) {
+    __shared__ int32_t s_id[MAXP * STEP_BLOCK];
+    __shared__ T s_poly[48 * STEP_BLOCK];
+    const int tid = threadIdx.x;
+    const uint32_t gen = *p.cur.gen;
+    const int32_t n = *p.defer_cnt;
+    for (int64_t qi = (int64_t)blockIdx.x * STEP_BLOCK + tid; qi < n; qi += (int64_t)gridDim.x * STEP_BLOCK) {
+        int32_t cell[3] = {INT32_MAX, 0, 0};
+        body_step<T, MAXP, 1, false, true>(p, true, p.defer_q[qi], 0, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
+                                           cell, gen, s_poly);
+    }
+    if (blockIdx.x == 0 && tid == 0) *p.defer_reset = 0;    // the next step's queue
+}
 // one wave per SIMD (up to 64 x 1024 owned bodies): every register is free
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
@@ -637,9 +666,10 @@ __global__ __launch_bounds__(STEP_BLOCK) void search_kernel(StepParams<T> p) {
     const T rad = p.cs.sx()[i];
     const uint32_t gen = *p.cur.gen;
     int32_t np_;
-    if constexpr (G == 1) np_ = search_partners<T, MAXP, false>(p, i, kind, x, rad, self.r, s_id, tid, gen);
+    bool defer = false;                          // split form: sphere worlds only
+    if constexpr (G == 1) np_ = search_partners<T, MAXP, false>(p, i, kind, x, rad, self.r, s_id, tid, gen, defer);
     else np_ = search_coop<T, MAXP, G, false>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
-                                       gen, [] {});
+                                       gen, defer, [] {});
     if (!active) return;
     for (int s = k; s < np_; s += G) p.plist[CHK((int64_t)s * p.S + l, (int64_t)MAXP * p.S)] = s_id[s * NB + slot];
     if (k == 0) p.plist_cnt[CHK(l, p.S)] = np_;
@@ -768,7 +798,7 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
     int64_t blocks = (p.n_local + nb - 1) / nb;
     if (blocks < 1) blocks = 1;
     const bool split = !coop && p.plist && !boxes;
-    if (boxes && !p.quat_cur) return hipErrorInvalidValue;
+    if (boxes && (!p.quat_cur || !p.defer_q || !p.defer_cnt || !p.defer_reset)) return hipErrorInvalidValue;
     // the cooperative search reads bucket slot snapshots: never launch it
     // on a table without them
     if (needs_slot_snapshots(coop, split) && (!p.cur.pos || (p.next.line && !p.next.pos))) return hipErrorInvalidValue;
@@ -778,15 +808,6 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
         if (maxp <= 16) hipLaunchKernelGGL((search_kernel<T, 16, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-    } else if (boxes) {
-        // box-capable forms (box scenes are small): cooperative or one-lane
-        if (coop) {
-            if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop_box<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-            else hipLaunchKernelGGL((step_kernel_coop_box<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        } else {
-            if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one_box<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-            else hipLaunchKernelGGL((step_kernel_one_box<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        }
     } else if (coop) {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
@@ -796,6 +817,12 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
     } else {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_one<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    }
+    if (boxes) {
+        const int64_t bb = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
+        const unsigned nbb = (unsigned)(bb < 1 ? 1 : bb > 256 ? 256 : bb);
+        if (maxp <= 16) hipLaunchKernelGGL((box_kernel<T, 16>), dim3(nbb), dim3(STEP_BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((box_kernel<T, 32>), dim3(nbb), dim3(STEP_BLOCK), 0, s, p);
     }
     return hipGetLastError();
 }

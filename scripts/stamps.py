@@ -8,13 +8,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rigidbody-simulation_amd"))
 CSRC = os.path.join(ROOT, "rigidbody-simulation_amd", "csrc")
 extra = os.environ.get("EXTRA_FLAGS", "")
-subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
-               f"-DRB_STAMPS=1 {extra} -o /tmp/libstamp.so rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True, check=True, cwd=CSRC)
+# a prebuilt stamps library (built on the CPU host, shipped with the tree) or build one here
+LIB = os.environ.get("STAMP_LIB", "/tmp/libstamp.so")
+if not os.path.exists(LIB):
+    subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
+                   f"-DRB_STAMPS=1 {extra} -o {LIB} rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True,
+                   check=True, cwd=CSRC)
 from rbhip import _lib, scenes
 import rbhip.world as W
-L = _lib.load("/tmp/libstamp.so")
+L = _lib.load(LIB)
 L.rb_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-for nx, ny, warm in [(64, 64, 300), (256, 256, 60), (1024, 1024, 60)]:
+sizes = [(64, 64, 300), (256, 256, 60), (1024, 1024, 60)]
+if os.environ.get("STAMP_SIZES"):        # e.g. "64x64,128x64,256x256"
+    sizes = [(int(a), int(b), 300) for a, b in (t.split("x") for t in os.environ["STAMP_SIZES"].split(","))]
+for nx, ny, warm in sizes:
     if nx * ny * (8 if nx * ny <= 20480 else 1) > 64 * (1 << 16): continue
     sc = scenes.flat_spheres(nx, ny, seed=0)
     G = 8 if sc.n <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "20480")) else 1
