@@ -630,7 +630,8 @@ void box_kernel(StepParams<T> p) {
     const int32_t n = *p.defer_cnt;
     for (int64_t qi = (int64_t)blockIdx.x * STEP_BLOCK + tid; qi < n; qi += (int64_t)gridDim.x * STEP_BLOCK) {
         int32_t cell[3] = {INT32_MAX, 0, 0};
-        body_step<T, MAXP, 1, false, true>(p, true, p.defer_q[qi], 0, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
+        // one lane per body: the lane's LDS column (partner list, polygon) is slot = tid
+        body_step<T, MAXP, 1, false, true>(p, true, p.defer_q[qi], tid, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
                                            cell, gen, s_poly);
     }
     if (blockIdx.x == 0 && tid == 0) *p.defer_reset = 0;    // the next step's queue
