@@ -278,6 +278,38 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     return np_;
 }
 
+// Wide form: the first WIDE_HPOS hits' snapshots stay in LDS (s_hpos, in
+// discovery order), so the solve does not gather them a second time;
+// s_didx maps a sorted list position to its discovery index (>= WIDE_HPOS:
+// gathered again).  RB_WIDE_LDSPOS=0: always gathered.
+#ifndef RB_WIDE_LDSPOS
+#define RB_WIDE_LDSPOS 1
+#endif
+constexpr int WIDE_HPOS = 8;
+
+template <int MAXP, typename T>
+__device__ __forceinline__ void list_insert_pos(int32_t *s_id, uint8_t *s_didx, Snap<T> *s_hpos, int stride, int slot,
+                                                int32_t &np_, int32_t &nh, int32_t j, const Snap<T> &sn,
+                                                bool &overflow) {
+    int pos = np_;
+    while (pos > 0) {
+        const int32_t prev = s_id[(pos - 1) * stride + slot];
+        if (prev == j) return;
+        if (prev < j) break;
+        --pos;
+    }
+    if (np_ >= MAXP) { overflow = true; return; }
+    for (int t = np_; t > pos; --t) {
+        s_id[t * stride + slot] = s_id[(t - 1) * stride + slot];
+        s_didx[t * stride + slot] = s_didx[(t - 1) * stride + slot];
+    }
+    s_id[pos * stride + slot] = j;
+    s_didx[pos * stride + slot] = (uint8_t)(nh < 255 ? nh : 255);
+    if (nh < WIDE_HPOS) s_hpos[nh * stride + slot] = sn;
+    ++nh;
+    ++np_;
+}
+
 // ---- wide one-lane search (one wave per SIMD, rb_kernels.hip step_kernel_wide)
 // A bucket head of 32 bytes: header and the first WIDE_HEAD_IDS ids.
 constexpr int WIDE_HEAD_IDS = 6;
@@ -303,8 +335,8 @@ template <int S> __device__ __forceinline__ uint32_t head6_id(const Head6 &h) {
 // the head loads.  Meant for one wave per SIMD: it holds many registers.
 template <typename T, int MAXP, typename Hit, typename Overlap>
 __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
-                                                       uint32_t *s_cand, int tid, uint32_t gen, Hit hit,
-                                                       Overlap overlap) {
+                                                       uint32_t *s_cand, uint8_t *s_didx, Snap<T> *s_hpos, int tid,
+                                                       uint32_t gen, Hit hit, Overlap overlap) {
     constexpr int NB = STEP_BLOCK;
     constexpr int QB = WIDE_QBATCH;
     int32_t cx, cy, cz, sx, sy, sz;
@@ -337,7 +369,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
         RB_WIDE_LIST(0) RB_WIDE_LIST(1) RB_WIDE_LIST(2) RB_WIDE_LIST(3) RB_WIDE_LIST(4) RB_WIDE_LIST(5)
 #undef RB_WIDE_LIST
     }
-    int32_t np_ = 0;
+    int32_t np_ = 0, nh = 0;
     bool overflow = false;
     for (int base = 0; base < n; base += QB) {
         uint32_t tj[QB];
@@ -351,7 +383,10 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
         }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
-            if (base + u < n && hit(tj[u], sn[u])) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+            if (base + u < n && hit(tj[u], sn[u])) {
+                if (RB_WIDE_LDSPOS) list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u], overflow);
+                else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+            }
     }
     STAMP(9);
     if (more) {
@@ -371,8 +406,12 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 }
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
-                    if (s0 + u < c[k] && hit(tj[u], sn[u]))
-                        list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+                    if (s0 + u < c[k] && hit(tj[u], sn[u])) {
+                        if (RB_WIDE_LDSPOS)
+                            list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u],
+                                                  overflow);
+                        else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+                    }
             }
         }
     }

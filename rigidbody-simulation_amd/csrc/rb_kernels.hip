@@ -148,10 +148,11 @@ __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32
 // K1, wide one-lane form (rb_grid.hpp search_buckets_wide)
 template <typename T, int MAXP, bool BOXES, typename Overlap>
 __device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
-                                                        T rad, T bi, int32_t *s_id, uint32_t *s_cand, int tid,
-                                                        uint32_t gen, bool &defer, Overlap overlap) {
+                                                        T rad, T bi, int32_t *s_id, uint32_t *s_cand, uint8_t *s_didx,
+                                                        Snap<T> *s_hpos, int tid, uint32_t gen, bool &defer,
+                                                        Overlap overlap) {
     return search_buckets_wide<T, MAXP>(
-        p, i, x, s_id, s_cand, tid, gen,
+        p, i, x, s_id, s_cand, s_didx, s_hpos, tid, gen,
         [&](uint32_t tj, const Snap<T> &s) { return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s, defer); },
         overlap);
 }
@@ -303,15 +304,17 @@ __device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T
 // already applied: forced), the Gauss-Seidel solves in canonical order,
 // integration, next-step insert.
 // The sorted partner list: ids at pid[u * stride] (an LDS column, or the
-// split form's per-slot list in HBM); snapshots at ppos[u * stride] (LDS,
-// POS = true: cooperative form) or gathered from the step-start snapshot.
-// POS is a template flag so LDS accesses stay ds_read (no flat loads).
-template <typename T, bool POS, bool BOXES = false>
+// split form's per-slot list in HBM); snapshots (PM, partner mode) at
+// ppos[u * stride] (LDS, PM = 1: cooperative form), at ppos[d * stride] for
+// the discovery index d = pdidx[u * stride] < WIDE_HPOS (LDS, PM = 2: wide
+// form) or gathered from the step-start snapshot (PM = 0, and PM = 2 past
+// WIDE_HPOS).  A template flag, so LDS accesses stay ds_read (no flat loads).
+template <typename T, int PM, bool BOXES = false>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, bool forced, LazyInvI<T> &invI,
                                             int32_t np_, const int32_t *pid, int64_t stride, const Snap<T> *ppos,
                                             int tid, int32_t *cell, uint32_t gen_next, T *poly = nullptr,
-                                            int ps = 0) {
+                                            int ps = 0, const uint8_t *pdidx = nullptr) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -363,8 +366,14 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (s0 + u >= np_) continue;
-            if constexpr (POS) pe[u] = ppos[(s0 + u) * stride];
-            else pe[u] = p.snap_cur[CHK(jj[u], p.n_global)];
+            if constexpr (PM == 1) {
+                pe[u] = ppos[(s0 + u) * stride];
+            } else if constexpr (PM == 2) {
+                const int d = pdidx[(s0 + u) * stride];
+                pe[u] = d < WIDE_HPOS ? ppos[d * stride] : p.snap_cur[CHK(jj[u], p.n_global)];
+            } else {
+                pe[u] = p.snap_cur[CHK(jj[u], p.n_global)];
+            }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -461,7 +470,8 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 template <typename T, int MAXP, int G, bool WIDE, bool BOXES>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
-                                          uint32_t *s_cand, int32_t *cell, uint32_t gen, T *s_poly) {
+                                          uint32_t *s_cand, int32_t *cell, uint32_t gen, T *s_poly,
+                                          uint8_t *s_didx = nullptr, Snap<T> *s_hpos = nullptr) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = p.lo + l;
@@ -489,7 +499,8 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     bool defer = false;                          // a box-involved partner in range: the box kernel steps it
     if constexpr (G == 1 && WIDE) {
         if (RB_ABLATE != 1)
-            np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, tid, gen, defer, [&] {
+            np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, s_didx, s_hpos, tid, gen,
+                                                       defer, [&] {
                 invI.get();
                 if (!p.xfrc) {
                     apply_force(p, l, in.m, invI, in.v, in.w);
@@ -521,8 +532,10 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
         invI.I = in.I;
         invI.q = in.q;
     }
-    body_update<T, (G > 1), BOXES>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB, s_pos + slot,
-                                   tid, cell, gen + 1u, BOXES ? s_poly + slot : nullptr, NB);
+    constexpr int PM = G > 1 ? 1 : (WIDE && RB_WIDE_LDSPOS) ? 2 : 0;
+    body_update<T, PM, BOXES>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB,
+                              PM == 2 ? s_hpos + slot : s_pos + slot, tid, cell, gen + 1u,
+                              BOXES ? s_poly + slot : nullptr, NB, PM == 2 ? s_didx + slot : nullptr);
 }
 
 // Halo exchange: fold the wave's new cells (cell[0] == INT32_MAX: none) into
@@ -556,6 +569,8 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     __shared__ int32_t s_id[MAXP * NB];
     __shared__ T s_poly[BOXES ? 48 * NB : 1];   // box-box face clipping: 2 x 8 vertices x 3 per body
     __shared__ uint32_t s_cand[WIDE ? WIDE_MAXC * NB : 1];
+    __shared__ uint8_t s_didx[WIDE ? MAXP * NB : 1];
+    __shared__ Snap<T> s_hpos[WIDE && RB_WIDE_LDSPOS ? WIDE_HPOS * NB : 1];
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
@@ -585,7 +600,7 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     int32_t cell[3] = {INT32_MAX, 0, 0};
     if (G > 1 || active)
         body_step<T, MAXP, G, WIDE, BOXES>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen,
-                                           s_poly);
+                                           s_poly, s_didx, s_hpos);
     if (p.bounds) fold_bounds(p.bounds, cell);
     if (late_publish && blockIdx.x == 0 && tid == 0) {
         if (p.next.line) *p.next.gen = gen + 1u;
@@ -696,8 +711,8 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
         invI.q = in.q;
         const int32_t np_ = p.plist_cnt[CHK(l, p.S)];
         if (RB_BOUNDS && np_ > 16) printf("RB_BOUNDS np_ %d at l %d\n", np_, l);
-        body_update<T, false>(p, l, i, x, kind, sz, self.r, in, false, invI, np_, p.plist + l, p.S, nullptr, tid,
-                              cell, gen_next);
+        body_update<T, 0>(p, l, i, x, kind, sz, self.r, in, false, invI, np_, p.plist + l, p.S, nullptr, tid,
+                          cell, gen_next);
     }
     if (p.bounds) fold_bounds(p.bounds, cell);
 }
