@@ -21,20 +21,24 @@ Scaling (body-id range shards, positions exchanged every step):
                     8 GPUs" on one 65,536-sphere scene; N = 1 is the BENCH line.
   weak              N patches of the config side by side on one shared
                     ground, one per rank (per-GPU work fixed).
-The ranks exchange positions inside the library every step (peer-to-peer
-over xGMI; halo pushes for slabs of >= rbhip.shard.HALO_MIN_SHARD bodies).
+The ranks exchange positions inside the library every step, peer-to-peer
+over xGMI, in one of two modes: halo pushes (each rank pushes to each peer
+only its bodies within a cell of the peer's bounds) or full slice reads.
+Both are warmed up, validated and timed over 20 steps on the node itself;
+the faster one runs the timed region (`config.exchange_probe_ms_per_step`
+lists both).  RCCL is the fallback when neither validates.
 
 N > 1 is validated: after the warmup and again after the timed region, every
 rank's bodies must be bit-identical (compared as uint64 words, so the sign
 of zeros counts) to one World of the whole scene stepped the same number of
-steps on rank 0's GPU.  A transport that fails the first check (or times
-out) is replaced by the next (p2p default -> p2p full reads -> rccl); one
-that fails the second makes the run exit non-zero instead of printing a
-number.
+steps on rank 0's GPU.  A mode that fails the first check (or times out) is
+dropped; a failure of the second makes the run exit non-zero instead of
+printing a number.
 
 value = total bodies x K / (max over ranks of the timed region), with the
-state resident in HBM.  The timed steps are steps W+K+1 .. W+2K from t = 0
-(the K steps before them capture the K-step graph): `timed_steps`.
+state resident in HBM.  The timed steps are steps D+K+1 .. D+2K from t = 0,
+D = W (+20 probe steps for N > 1); the K steps before them capture the
+K-step graph: `timed_steps`.
 roofline: algorithmic HBM bytes of the step kernel (248 B per
 sphere body-step in fp64) x owned bodies / its average launch duration.
 One rank: HIP events recorded on the world's stream (torch's current
@@ -279,22 +283,50 @@ def main():
 
     scene, desc = make_scene(args.config, P, args.scaling)
     check = SingleWorldCheck(scene, args.dtype, device, rank, P) if P > 1 else None
-    # (transport, halo): the library's default (peer-to-peer, halo for large
-    # shards), then peer-to-peer full reads, then RCCL
-    transports = [(None, "auto"), ("p2p", False), ("rccl", "auto")] if P > 1 else [(None, "auto")]
-    for k, (tr, halo) in enumerate(transports):
-        sw = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo)
-        # warmup (also builds and caches the K-step graphs)
+    dev_red = f"cuda:{device}" if backend == "nccl" else "cpu"
+
+    def probe_ms(sw) -> float:
+        """Max over ranks of PROBE steps' wall time (barrier on both sides)."""
+        sw.sync(); torch.cuda.synchronize(); dist.barrier()
+        t0 = time.perf_counter()
+        sw.step(PROBE)
+        sw.sync(); torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], device=dev_red, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) * 1e3 / PROBE
+
+    # N > 1: both peer-to-peer modes (halo pushes, full slice reads) are
+    # warmed up, validated against one World and timed over PROBE steps on
+    # this node's xGMI; the faster valid one runs the timed region.  RCCL is
+    # the fallback when neither validates.
+    PROBE = 20
+    done = args.warmup
+    if P == 1:
+        sw = ShardedWorld(scene, dtype=args.dtype, device=device)
         sw.step(args.warmup)
-        if check is None or check(sw, args.warmup):
-            break
-        name = sw.transport + (" (halo)" if sw.halo else "")
-        sw.world.close()
-        if k + 1 == len(transports):
-            raise SystemExit(f"bench: every transport failed validation (last: {name})")
-        if rank == 0:
-            print(f"bench: {name} exchange failed validation; falling back to {transports[k + 1][0]}"
-                  f"{'' if transports[k + 1][1] else ' (full reads)'}", file=sys.stderr, flush=True)
+        probes = {}
+    else:
+        cands, probes = [], {}
+        for tr, halo in (("p2p", True), ("p2p", False), ("rccl", "auto")):
+            if tr == "rccl" and cands:
+                break
+            c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo)
+            name = c.transport + (" halo" if c.halo else " full reads" if c.transport == "p2p" else "")
+            c.step(args.warmup)
+            if not check(c, args.warmup):
+                if rank == 0:
+                    print(f"bench: {name} exchange failed validation", file=sys.stderr, flush=True)
+                c.world.close()
+                continue
+            probes[name] = probe_ms(c)
+            cands.append((probes[name], name, c))
+        if not cands:
+            raise SystemExit("bench: every transport failed validation")
+        cands.sort(key=lambda t: t[0])
+        sw = cands[0][2]
+        for _, _, c in cands[1:]:
+            c.world.close()
+        done = args.warmup + PROBE
     w = sw.world
     sw.sync()
 
@@ -316,12 +348,12 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
-    timed = [args.warmup + args.steps + 1, args.warmup + 2 * args.steps]
+    timed = [done + args.steps + 1, done + 2 * args.steps]
     if P > 1:
-        t = torch.tensor([elapsed], device=f"cuda:{device}" if backend == "nccl" else "cpu", dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev_red, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        if not check(sw, args.warmup + 2 * args.steps):
+        if not check(sw, done + 2 * args.steps):
             raise SystemExit("bench: the sharded run diverged from the single-World run during the timed steps")
 
     # roofline: average step-kernel launch duration.  One rank: the timed
@@ -361,7 +393,8 @@ def main():
                    "timed_steps": timed,
                    "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction,
                    **({"validated": f"bit-identical (uint64 words) to one World of the whole scene after "
-                                    f"{args.warmup} and {args.warmup + 2 * args.steps} steps"} if P > 1 else {})},
+                                    f"{args.warmup} and {done + 2 * args.steps} steps",
+                       "exchange_probe_ms_per_step": probes} if P > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": traffic_lower,
                      "traffic_source": traffic_src,
