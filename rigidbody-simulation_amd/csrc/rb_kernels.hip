@@ -456,7 +456,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     wt_store(p.st.wx() + l, w.x); wt_store(p.st.wy() + l, w.y); wt_store(p.st.wz() + l, w.z);
     wt_store(p.st.qw() + l, qn.w); wt_store(p.st.qx() + l, qn.x); wt_store(p.st.qy() + l, qn.y);
     wt_store(p.st.qz() + l, qn.z);
-    if (BOXES && kind != 0) {                   // next step's orientation snapshot
+    // next step's orientation snapshot (box worlds), from every kernel that
+    // steps a box: the box kernel reads it for a partner that was out of any
+    // box pair's range (stepped by a sphere kernel) in the step before
+    if (p.quat_next && kind != 0) {
         T *qs = p.quat_next + 4 * (int64_t)i;
         wt_store(qs + 0, qn.w); wt_store(qs + 1, qn.x); wt_store(qs + 2, qn.y); wt_store(qs + 3, qn.z);
     }

@@ -102,3 +102,46 @@ def test_box_pile_f32_bit_exact(rb, oracle):
         w.step(300)
         q, v = w.get_state()
     assert np.array_equal(q, q0) and np.array_equal(v, v0)
+
+
+def _approaching_boxes():
+    """Two spinning cubes and a sphere thrown at each other in the air: for
+    the first 7 steps no box-involved pair is within bounding range (the
+    sphere step kernel steps the cubes), then the cubes meet face to face in
+    the very step their bounding spheres first overlap (the box kernel takes
+    them over and reads both step-start orientations)."""
+    from rbhip import scenes
+    h = 0.4
+    kind = np.array([1, 1, 0], np.int32)
+    mass = np.array([scenes.M_CUBE_H04, scenes.M_CUBE_H04, scenes.M_SPHERE_R02])
+    inertia = np.array([[scenes.I_CUBE_H04] * 3, [scenes.I_CUBE_H04] * 3, [scenes.I_SPHERE_R02] * 3])
+    size = np.array([[h, h, h], [h, h, h], [0.2, 0, 0]])
+    qpos = np.array([[-2.5, 0.0, 3.0, 1, 0, 0, 0], [2.5, 0.1, 3.0, 1, 0, 0, 0], [0.1, 2.2, 3.1, 1, 0, 0, 0]], float)
+    qvel = np.array([[30.0, 0, 0, 1.0, 2.0, 0.5], [-30.0, 0, 0, -0.5, 1.0, 2.0], [0, -3.5, 0, 0, 0, 0]], float)
+    return scenes.Scene("approaching_boxes", kind, mass, inertia, size, np.array([[0.0, 0, 1, 0, 0, 0]]),
+                        qpos, qvel, dt=0.01, restitution=0.5, friction=0.4, threshold=0.0)
+
+
+@pytest.mark.parametrize("form,env", [("coop", {}), ("one", {"RBHIP_COOP_MAX_BODIES": "0"})])
+def test_boxes_entering_range_bit_exact(rb, oracle, monkeypatch, form, env):
+    """Boxes stepped by the sphere kernel (no box partner in range) must
+    still publish their orientation for the step a box pair comes into
+    range: every step's contacts and state bit-exact with the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = _approaching_boxes()
+    osc = oracle.OracleScene(sc, max_partners=32)
+    q, v = sc.qpos0, sc.qvel0
+    kinds = set()
+    with rb.World(sc, max_partners=32) as w:
+        w.record_contacts(True)
+        for s in range(1, 151):
+            q, v, (cnt, par, kin, dis) = oracle.step(osc, q, v, 1, record=True)
+            w.step(1)
+            gc, gp, gk, gd = w.contacts()
+            assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin), \
+                f"contacts differ at step {s}"
+            gq, gv = w.get_state()
+            assert _same(gq, q) and _same(gv, v), f"state differs at step {s}"
+            kinds |= set(kin.tolist())
+    assert {32, 40} <= kinds, kinds
