@@ -133,8 +133,12 @@ template <typename T> __device__ M3<T> inertia_world(V3<T> I, Q4<T> q) {
 // Returns false (and leaves v, w untouched) when the contact separates
 // (u_rel_n >= 0: the reference's zero impulse changes nothing but the sign
 // of zeros).  jn/jt are exported for the KAT entry.
+// k = 1/m + 1/18 (collision.py:35): a body constant, evaluated
+// once per body-step instead of once per contact (the same value)
+template <typename T> __device__ __forceinline__ T impulse_k(T m) { return (T(1) / m) + (T(1) / T(18)); }
+
 template <typename T>
-__device__ __forceinline__ bool impulse(T m, V3<T> v, V3<T> w, V3<T> r, V3<T> n, T e, T mu,
+__device__ __forceinline__ bool impulse(T k, V3<T> v, V3<T> w, V3<T> r, V3<T> n, T e, T mu,
                                         T& jn_out, V3<T>& jt_out) {
     const V3<T> c = np_cross(w, r);
     const V3<T> u = {v.x + c.x, v.y + c.y, v.z + c.z};
@@ -142,7 +146,6 @@ __device__ __forceinline__ bool impulse(T m, V3<T> v, V3<T> w, V3<T> r, V3<T> n,
     const V3<T> ut = {u.x - un * n.x, u.y - un * n.y, u.z - un * n.z};
     jt_out = {T(0), T(0), T(0)};
     if (un >= T(0)) { jn_out = T(0); return false; }
-    const T k = (T(1) / m) + (T(1) / T(18));
     const T jn = (-(T(1) + e) * un) / k;
     const T nut = sqroot(np_dot(ut, ut));
     if (nut > T(1e-6)) {

@@ -340,7 +340,11 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     constexpr int NB = STEP_BLOCK;
     constexpr int QB = WIDE_QBATCH;
     int32_t cx, cy, cz, sx, sy, sz;
-    if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) { atomicOr(p.err, ERR_DOMAIN); return 0; }
+    if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) {
+        atomicOr(p.err, ERR_DOMAIN);
+        overlap();                                // (on both paths: measured 2-4 % faster at 32k-65k bodies)
+        return 0;
+    }
     uint32_t b[8];
     int32_t c[8];
     Head6 hd[8];
@@ -371,7 +375,11 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     }
     int32_t np_ = 0, nh = 0;
     bool overflow = false;
-    for (int base = 0; base < n; base += QB) {
+    // candidates WIDE_QBATCH at a time; the first batch is issued by every
+    // lane (padding = the body itself, which loads nothing): measured 2-7 %
+    // faster at 32k-65k bodies than a loop all of whose batches are
+    // conditional on the lane's candidate count
+    auto batch = [&](int base) {
         uint32_t tj[QB];
         Snap<T> sn[QB];
 #pragma unroll
@@ -387,7 +395,9 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 if (RB_WIDE_LDSPOS) list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u], overflow);
                 else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
             }
-    }
+    };
+    batch(0);
+    for (int base = QB; base < n; base += QB) batch(base);
     STAMP(9);
     if (more) {
         // buckets of 7+ bodies: the remaining ids from their lines, QB at a time

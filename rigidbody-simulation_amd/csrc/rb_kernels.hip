@@ -100,13 +100,13 @@ template <typename T> struct LazyInvI {
 // one contact of body i through the reference's skip rules then K2
 template <typename T>
 __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Contact<T> &con, V3<T> x, V3<T> n,
-                                              T m, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
+                                              T m, T k, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
     if (!(con.dist < T(0))) return;                 // collision.py:74 (NaN fails too)
     if (absval(con.dist) < p.thr) return;           // collision.py:79-80
     const V3<T> r = {con.pos.x - x.x, con.pos.y - x.y, con.pos.z - x.z};   // :75
     T jn;
     V3<T> jt;
-    if (impulse(m, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
+    if (impulse(k, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
 }
 
 // Candidate test shared by every search form: true if the candidate with
@@ -322,6 +322,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 
     // ---- a4: gravity / applied force (collision.py:66-70) ------------------
     if (!forced) apply_force(p, l, m, invI, v, w);
+    const T k = impulse_k(m);
 
     STAMP(3);
     int32_t nrec = 0;
@@ -333,7 +334,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             Contact<T> con;
             if (!plane_sphere(pn, pp, x, sz.x, con)) continue;
             record(p, l, nrec, -1 - pl, 0, con.dist);
-            solve_contact(p, con, x, con.frame, m, invI, v, w);
+            solve_contact(p, con, x, con.frame, m, k, invI, v, w);
         }
     }
     M3<T> M;                                       // box orientation (mj_kinematics of the free joint)
@@ -349,7 +350,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                 if (!plane_box_corner(pn, x, dist, M, sz, c, con)) continue;
                 ++cnt;
                 record(p, l, nrec, -1 - pl, 1 + c, con.dist);
-                solve_contact(p, con, x, con.frame, m, invI, v, w);
+                solve_contact(p, con, x, con.frame, m, k, invI, v, w);
             }
         }
     }
@@ -390,7 +391,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                         record(p, l, nrec, j, ck, con.dist);
                         const V3<T> n = (p.oriented && self_g1) ? V3<T>{-con.frame.x, -con.frame.y, -con.frame.z}
                                                                 : con.frame;
-                        solve_contact(p, con, x, n, m, invI, v, w);
+                        solve_contact(p, con, x, n, m, k, invI, v, w);
                     };
                     M3<T> Mj;
                     const V3<T> hj = {p.cs.sx()[j], p.cs.sy()[j], p.cs.sz()[j]};
@@ -426,7 +427,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                 n = con.frame;
             }
             record(p, l, nrec, j, 16, con.dist);
-            solve_contact(p, con, x, n, m, invI, v, w);
+            solve_contact(p, con, x, n, m, k, invI, v, w);
         }
     }
     if (p.rec_count) p.rec_count[l] = nrec;
@@ -491,7 +492,9 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     BodyIn<T> in;
     LazyInvI<T> invI;
     bool forced = false;
-    constexpr bool early = G > 1 || WIDE;       // state loads issued before the search
+    // state loads issued before the search (the wide form measured 5 % slower
+    // with them issued after the bucket heads, C3)
+    constexpr bool early = G > 1 || WIDE;
     if constexpr (early) {
         in = load_body(p, l, i);
         invI.I = in.I;
@@ -740,7 +743,7 @@ __global__ void kat_impulse_kernel(int64_t n, const double *in, double *out) {
     const M3<T> invI = np_inv3(Iw);
     T jn;
     V3<T> jt;
-    impulse(m, v, w, r, nn, e, mu, jn, jt);
+    impulse(impulse_k(m), v, w, r, nn, e, mu, jn, jt);
     apply(v, w, m, invI, r, nn, jn, jt);      // the reference always applies
     double *o = out + 10 * c;
     o[0] = jn; o[1] = jt.x; o[2] = jt.y; o[3] = jt.z;

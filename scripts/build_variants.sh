@@ -12,7 +12,7 @@ mkdir -p "$ROOT/build"
 rm -f "$ROOT"/build/*.so
 TMP=$(mktemp -d)
 mkdir -p "$TMP/rigidbody-simulation_amd/csrc" "$TMP/include"
-for f in $SRCS rb_device.hpp rb_grid.hpp rb_internal.hpp; do
+for f in $SRCS rb_device.hpp rb_grid.hpp rb_internal.hpp rb_boxes.hpp; do
   git -C "$ROOT" show "$REF:rigidbody-simulation_amd/csrc/$f" > "$TMP/rigidbody-simulation_amd/csrc/$f"
 done
 git -C "$ROOT" show "$REF:include/rbhip.h" > "$TMP/include/rbhip.h"
