@@ -238,6 +238,8 @@ template <typename T> struct HaloParams {
 enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2 };
 // boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
+// the wide form's kernel alone (its own translation unit: scheduled for memory clauses)
+template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip

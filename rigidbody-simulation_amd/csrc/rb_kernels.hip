@@ -585,8 +585,12 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     STAMP(0);
     // one scalar round trip for the prologue's kernel arguments (the
     // scheduler would otherwise issue the second load after the first wait)
+    // (the table generations' addresses and the next table's too: loaded on
+    // their own, each after a wait for the one before, they held the
+    // own-snapshot loads back two more scalar round trips in the one-lane
+    // forms)
     asm volatile("" ::"s"(p.snap_cur), "s"(p.st.base), "s"(p.st.S), "s"(p.cs.base), "s"(p.cs.Npad), "s"(p.cs.kind),
-                 "s"(p.n_local), "s"(p.lo));
+                 "s"(p.n_local), "s"(p.lo), "s"(p.cur.gen), "s"(p.next.line), "s"(p.next.gen), "s"(p.epoch));
 
     // Block 0 advances the exchange's step number and publishes the next
     // table's generation (one more than the one this step reads) for the
@@ -595,7 +599,6 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     // pass it), which cost its waves a scalar round trip (+11 % at 16k
     // bodies).  The one-lane forms measured no gain (65k) or a loss (1M).
     constexpr bool late_publish = G > 1;
-    if constexpr (late_publish) asm volatile("" ::"s"(p.cur.gen));   // with the prologue's scalar loads
     if (!late_publish && p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;
     const uint32_t gen = *p.cur.gen;
     if (!late_publish && p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
@@ -834,8 +837,8 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     } else if (form == FORM_WIDE) {
-        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        const hipError_t we = launch_step_wide<T>(p, maxp, s);
+        if (we != hipSuccess) return we;
     } else {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((step_kernel_one<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
@@ -880,12 +883,31 @@ template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, 
     return hipGetLastError();
 }
 
+template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, hipStream_t s) {
+    int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
+    if (blocks < 1) blocks = 1;
+    if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    return hipGetLastError();
+}
+
 // explicit instantiations: RB_INST bit 1 = fp64, bit 2 = fp32 (the Makefile
-// builds the two halves as separate objects, in parallel)
+// builds the two halves as separate objects, in parallel); RB_WIDE_UNIT: the
+// wide form's kernel only (compiled with its own scheduling flags), else
+// everything else
 #ifndef RB_INST
 #define RB_INST 3
 #endif
-#if RB_INST & 1
+#ifndef RB_WIDE_UNIT
+#define RB_WIDE_UNIT 2                  // both (a one-command build of all sources)
+#endif
+#if RB_WIDE_UNIT >= 1 && (RB_INST & 1)
+template hipError_t launch_step_wide<double>(const StepParams<double> &, int, hipStream_t);
+#endif
+#if RB_WIDE_UNIT >= 1 && (RB_INST & 2)
+template hipError_t launch_step_wide<float>(const StepParams<float> &, int, hipStream_t);
+#endif
+#if RB_WIDE_UNIT != 1 && (RB_INST & 1)
 template hipError_t launch_step<double>(const StepParams<double> &, int, int, bool, hipStream_t);
 template hipError_t launch_kat_narrow<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
@@ -893,7 +915,7 @@ template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *
 template hipError_t launch_kat_inertia<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
 #endif
-#if RB_INST & 2
+#if RB_WIDE_UNIT != 1 && (RB_INST & 2)
 template hipError_t launch_step<float>(const StepParams<float> &, int, int, bool, hipStream_t);
 template hipError_t launch_kat_narrow<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
