@@ -11,7 +11,8 @@ from rbhip import scenes
 from rbhip.shard import wrap_gpos
 
 K = 400
-sc = scenes.make(os.environ.get("CFG", "c2"))
+sc = (scenes.flat_spheres(int(os.environ["NX"]), int(os.environ["NY"])) if os.environ.get("NX")
+      else scenes.make(os.environ.get("CFG", "c2")))
 
 
 def timed(fn):
