@@ -583,6 +583,13 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     const int tid = threadIdx.x;
     if (RB_ABLATE == 3) return;
     STAMP(0);
+#if RB_STAMPS
+    // placement: HW_ID (wave, SIMD, CU, SE fields) and XCC_ID of the block's first wave
+    if (tid == 0 && blockIdx.x < (1u << 16)) {
+        rb_stamp_buf[blockIdx.x][15] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        rb_stamp_buf[blockIdx.x][14] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+#endif
     // one scalar round trip for the prologue's kernel arguments (the
     // scheduler would otherwise issue the second load after the first wait)
     // (the table generations' addresses and the next table's too: loaded on
