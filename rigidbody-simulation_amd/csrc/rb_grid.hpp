@@ -96,11 +96,17 @@ __device__ __forceinline__ uint32_t bucket_hash(int32_t ix, int32_t iy, int32_t 
     h ^= h >> 16;
     return h;
 }
+// Grid::super packs the group shape: x, y, z bits in nibbles 0, 1, 2 (0x111
+// = the 2x2x2 super-cells; 0 = one hash per cell).
 template <typename T>
 __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, const Grid<T> &g) {
     if (g.super) {
-        const uint32_t sc = bucket_hash(ix >> 1, iy >> 1, iz >> 1) & (g.hmask >> 3);   // arithmetic: floor(c/2)
-        return (sc << 3) | (uint32_t)((ix & 1) | ((iy & 1) << 1) | ((iz & 1) << 2));
+        const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
+        // arithmetic shifts: floor(c / 2^b)
+        const uint32_t sc = bucket_hash(ix >> bx, iy >> by, iz >> bz) & (g.hmask >> gb);
+        const uint32_t in = (uint32_t)(ix & ((1 << bx) - 1)) | ((uint32_t)(iy & ((1 << by) - 1)) << bx) |
+                            ((uint32_t)(iz & ((1 << bz) - 1)) << (bx + by));
+        return (sc << gb) | in;
     }
     return bucket_hash(ix, iy, iz) & g.hmask;
 }

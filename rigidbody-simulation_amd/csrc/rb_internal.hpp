@@ -104,7 +104,7 @@ template <typename T> struct Grid {
     T inv_cs;                          // 1 / cell size
     uint32_t hmask;                    // H - 1 (H power of two)
     int32_t H;
-    int32_t super;                     // buckets grouped by 2x2x2 super-cell (rb_grid.hpp bucket_of)
+    int32_t super;                     // buckets grouped by super-cell, shape in nibbles (rb_grid.hpp bucket_of)
 };
 
 template <typename T> struct StepParams {

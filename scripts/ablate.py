@@ -62,7 +62,8 @@ for rnd in range(2):
             for name, val in assigns:
                 os.environ[name] = val
             for nx, ny in sizes:
-                sc = scenes.flat_spheres(nx, ny, seed=0)
+                sc = (scenes.incline_spheres(nx, ny, seed=0) if os.environ.get("SCENE") == "incline"
+                      else scenes.flat_spheres(nx, ny, seed=0))
                 try:
                     avg = run_one(sc)
                 except _lib.RbError as e:        # a diagnostic build may produce garbage
