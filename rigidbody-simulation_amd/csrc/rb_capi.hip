@@ -713,20 +713,34 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     int64_t hmax = 4096;
     while (hmax * 2 * per_bucket <= cap_bytes && hmax < (int64_t(1) << 26)) hmax *= 2;
     w->H = next_pow2(want) < hmax ? next_pow2(want) : hmax;
-    // the one-lane and wide forms hash 16x16x4-cell groups, the buckets of a
-    // group contiguous (128 KB of lines): measured 7 % faster at 65k bodies
-    // (flat), 2 % at 65k (incline) and 1M, 3 % at 32k than a hash per cell,
-    // and than the 2x2x2 super-cells.  The cooperative form keeps
-    // a hash per cell (no change measured).  RBHIP_HASH_GROUP=bx:by:bz
-    // (group of 2^bx x 2^by x 2^bz cells) overrides.
-    w->group = coop_world ? 0 : 0x244;
+    // The one-lane and wide forms group cells 8x8x4, the buckets of a group
+    // contiguous (32 KB of lines), and lay the groups out linearly, periodic
+    // in 2^lx x 2^ly x 2^lz groups (below): against a hash per cell measured
+    // 6 % faster at 65k bodies (flat), 5 % (incline), 12 % at 1M; hashed
+    // groups were bimodal (a group collision doubles the bodies of every
+    // bucket in both groups and sends waves through the wide form's extra
+    // round trip for buckets of 7+ ids).  The cooperative form
+    // keeps a hash per cell.  RBHIP_HASH_GROUP=bx:by:bz (hashed groups of
+    // 2^bx x 2^by x 2^bz cells) or bx:by:bz:l (linear) overrides.
+    w->group = coop_world ? 0 : 0x233;
+    bool linear = !coop_world;
     if (const char *ev = getenv("RBHIP_HASH_GROUP")) {
         int bx = 0, by = 0, bz = 0;
-        if (sscanf(ev, "%d:%d:%d", &bx, &by, &bz) == 3 && bx >= 0 && by >= 0 && bz >= 0 && bx + by + bz <= 12)
+        char mode = 'h';
+        if (sscanf(ev, "%d:%d:%d:%c", &bx, &by, &bz, &mode) >= 3 && bx >= 0 && by >= 0 && bz >= 0 && bx + by + bz <= 12)
             w->group = bx | (by << 4) | (bz << 8);
+        linear = mode == 'l';      // bx:by:bz hashed, bx:by:bz:l linear
     }
     while (w->group && (int64_t(1) << ((w->group & 15) + ((w->group >> 4) & 15) + ((w->group >> 8) & 15))) > w->H / 4)
         w->group = 0;              // a table too small for the groups: one hash per cell
+    if (w->group && linear) {
+        // the group slots split into a period of 2^lx x 2^ly x 2^lz groups (z: at most 8)
+        int lg = 0;
+        while ((int64_t(1) << (lg + 1)) <= w->H) ++lg;
+        lg -= (w->group & 15) + ((w->group >> 4) & 15) + ((w->group >> 8) & 15);
+        const int lz = lg / 3 < 3 ? lg / 3 : 3, lx = (lg - lz + 1) / 2, ly = lg - lz - lx;
+        w->group |= (lx << 12) | (ly << 16) | (lz << 20) | (1 << 24);
+    }
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
     // algorithmic bytes per body-step: 13 state reals read + 13

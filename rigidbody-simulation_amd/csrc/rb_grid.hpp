@@ -97,13 +97,26 @@ __device__ __forceinline__ uint32_t bucket_hash(int32_t ix, int32_t iy, int32_t 
     return h;
 }
 // Grid::super packs the group shape: x, y, z bits in nibbles 0, 1, 2 (0x111
-// = the 2x2x2 super-cells; 0 = one hash per cell).
+// = the 2x2x2 super-cells; 0 = one hash per cell).  Bit 24 set: groups are
+// laid out linearly, periodic in 2^lx x 2^ly x 2^lz groups (lx, ly, lz in
+// nibbles 3, 4, 5), instead of hashed — no two groups within one period
+// share buckets (hashed groups of a compact scene collide with a birthday
+// probability near 1, and a collision doubles the bodies of every bucket in
+// both groups).
 template <typename T>
 __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, const Grid<T> &g) {
     if (g.super) {
         const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
         // arithmetic shifts: floor(c / 2^b)
-        const uint32_t sc = bucket_hash(ix >> bx, iy >> by, iz >> bz) & (g.hmask >> gb);
+        const int32_t gx = ix >> bx, gy = iy >> by, gz = iz >> bz;
+        uint32_t sc;
+        if (g.super >> 24) {
+            const int lx = (g.super >> 12) & 15, ly = (g.super >> 16) & 15, lz = (g.super >> 20) & 15;
+            sc = ((uint32_t)gx & ((1u << lx) - 1u)) | (((uint32_t)gy & ((1u << ly) - 1u)) << lx) |
+                 (((uint32_t)gz & ((1u << lz) - 1u)) << (lx + ly));
+        } else {
+            sc = bucket_hash(gx, gy, gz) & (g.hmask >> gb);
+        }
         const uint32_t in = (uint32_t)(ix & ((1 << bx) - 1)) | ((uint32_t)(iy & ((1 << by) - 1)) << bx) |
                             ((uint32_t)(iz & ((1 << bz) - 1)) << (bx + by));
         return (sc << gb) | in;

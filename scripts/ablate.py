@@ -62,7 +62,9 @@ for rnd in range(2):
             for name, val in assigns:
                 os.environ[name] = val
             for nx, ny in sizes:
-                sc = (scenes.incline_spheres(nx, ny, seed=0) if os.environ.get("SCENE") == "incline"
+                kind = os.environ.get("SCENE", "flat")
+                sc = (scenes.incline_spheres(nx, ny, seed=0) if kind == "incline"
+                      else scenes.incline_cubes(nx, ny, seed=0) if kind == "cubes"
                       else scenes.flat_spheres(nx, ny, seed=0))
                 try:
                     avg = run_one(sc)

@@ -13,6 +13,11 @@ if [ -n "${ENVS:-}" ]; then
   LIBS=rigidbody-simulation_amd/rbhip/librbhip.so ENVS="$ENVS" SIZES="${SIZES:-64x64,128x64,256x256,512x512}" \
     timeout -k 10 600 python scripts/ablate.py > gpurun_out/envab.txt 2>&1
   rc=$?; grep "N=" gpurun_out/envab.txt || tail gpurun_out/envab.txt; [ $rc -eq 0 ] || exit $rc
+  if [ -n "${CUBE_SIZES:-}" ]; then
+    SCENE=cubes LIBS=rigidbody-simulation_amd/rbhip/librbhip.so ENVS="$ENVS" SIZES="$CUBE_SIZES" \
+      timeout -k 10 600 python scripts/ablate.py > gpurun_out/envab_cubes.txt 2>&1
+    rc=$?; echo "cubes:"; grep "N=" gpurun_out/envab_cubes.txt || tail gpurun_out/envab_cubes.txt; [ $rc -eq 0 ] || exit $rc
+  fi
   if [ -n "${INCLINE_SIZES:-}" ]; then
     SCENE=incline LIBS=rigidbody-simulation_amd/rbhip/librbhip.so ENVS="$ENVS" SIZES="$INCLINE_SIZES" \
       timeout -k 10 600 python scripts/ablate.py > gpurun_out/envab_incline.txt 2>&1
