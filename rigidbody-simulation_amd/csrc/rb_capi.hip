@@ -692,14 +692,14 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxrec = 4 * w->n_planes + (any_box ? 4 : 1) * w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
-    // per-cell hash, sized so few cells share a bucket and few false
-    // candidates are read: cooperative worlds (which also keep a slot
-    // snapshot line per bucket) 16 buckets per body; the one-lane and wide
-    // forms max(32 per body, 2^23) (measured against 16 per body: -8 % at
-    // 65,536 bodies, -2 % at 262k and 1M; 4 per body was 15 % slower than
-    // 16).  At most 2^26 buckets (8 GB of lines per table).
+    // buckets: cooperative worlds (a hash per cell; they also keep a slot
+    // snapshot line per bucket) 16 per body; the one-lane and wide forms
+    // (linear cell groups, below) 32 per body, so the groups' period spans
+    // the scene (C3: 2^21 buckets, 205 m x 102 m x 12.8 m; as fast as 2^23,
+    // 16 per body 20 % slower: the period then folds the scene onto itself).
+    // At most 2^26 buckets (8 GB of lines per table).
     const bool coop_world = w->n_local <= w->coop_max;
-    int64_t want = coop_world ? 16 * w->N : (32 * w->N > (int64_t(1) << 23) ? 32 * w->N : (int64_t(1) << 23));
+    int64_t want = coop_world ? 16 * w->N : 32 * w->N;
     if (const char *ev = getenv("RBHIP_HASH_FACTOR"))
         if (atoll(ev) > 0) want = atoll(ev) * w->N;
     if (want < 4096) want = 4096;
