@@ -21,7 +21,7 @@ WARM, K = int(os.environ.get("WARM", "450")), int(os.environ.get("K", "200"))
 stream = torch.cuda.current_stream().cuda_stream
 print(f"| P | owned bodies per rank | form | step kernel us, slowest rank (steps {WARM + 1}-{WARM + K}) | mean over ranks |")
 print("|---|---|---|---|---|")
-for P in (1, 2, 4, 8):
+for P in [int(v) for v in os.environ.get("PS", "1,2,4,8").split(",")]:
     ws = [rbhip.World(sc, rank=r, world_size=P) for r in range(P)]
     for w in ws:
         w.set_stream(stream)
