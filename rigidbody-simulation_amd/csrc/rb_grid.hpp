@@ -141,29 +141,44 @@ __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, in
 // stale header to (gen, 0), a returning atomicAdd claims the slot
 // (claim_slot); the slot is then written (publish_slot).  Split so a caller
 // can put independent work between the two and hide the atomic's round trip.
-struct Claim { uint32_t b; int32_t slot; };      // slot < 0: not inserted
+// The Claim keeps the atomic's raw return value and decodes the slot only in
+// publish_slot: decoding it in claim_slot, at the join of the caller's
+// branches around the claim, made the compiler wait for the atomic right
+// there, ahead of all the work placed between the two.
+struct Claim {
+    uint32_t b;
+    int32_t ok;                  // 0: not inserted (no table, or a non-finite position)
+    unsigned long long old;      // the header before this claim (valid if ok)
+    uint32_t gen;
+};
 template <typename T>
 __device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
                                             uint32_t gen) {
-    int32_t ix, iy, iz;
-    if (!cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz)) { atomicOr(err, ERR_DOMAIN); return {0u, -1}; }
+    int32_t ix = 0, iy = 0, iz = 0;
+    const bool in = cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz);
+    if (!in) atomicOr(err, ERR_DOMAIN);
     const uint32_t b = bucket_of(ix, iy, iz, g);
-    auto *h = reinterpret_cast<unsigned long long *>(tab.line + (int64_t)CHK(b, g.H) * LINE_WORDS);
-    atomicMax(h, (unsigned long long)gen << 32);
-    const unsigned long long old = atomicAdd(h, 1ull);
-    // after the max the header carries gen (no later generation writes this
-    // table before the next step's launch)
-    const int32_t slot = (uint32_t)(old >> 32) == gen ? (int32_t)(uint32_t)old : BUCKET_SLOTS;
-    return {b, slot};
+    // no defined value when !in (never decoded then): a constant here would
+    // make the join select it against the atomic's return, i.e. wait for it
+    unsigned long long old = __builtin_nondeterministic_value(0ull);
+    if (in) {
+        auto *h = reinterpret_cast<unsigned long long *>(tab.line + (int64_t)CHK(b, g.H) * LINE_WORDS);
+        atomicMax(h, (unsigned long long)gen << 32);
+        old = atomicAdd(h, 1ull);
+    }
+    return {b, in ? 1 : 0, old, gen};
 }
 template <typename T>
 __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
                                              uint32_t tagged_id) {
-    if (c.slot < 0) return;
-    if (c.slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    const int64_t o = CHK((int64_t)c.b * LINE_WORDS + HEAD_WORDS + c.slot, RB_BOUNDS ? 1ll << 40 : 0);
+    if (!c.ok) return;
+    // after the max the header carries gen (no later generation writes this
+    // table before the next step's launch)
+    const int32_t slot = (uint32_t)(c.old >> 32) == c.gen ? (int32_t)(uint32_t)c.old : BUCKET_SLOTS;
+    if (slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    const int64_t o = CHK((int64_t)c.b * LINE_WORDS + HEAD_WORDS + slot, RB_BOUNDS ? 1ll << 40 : 0);
     wt_store(tab.line + o, tagged_id);
-    if (tab.pos) wt_store(tab.pos + (int64_t)c.b * LINE_WORDS + c.slot, sn);
+    if (tab.pos) wt_store(tab.pos + (int64_t)c.b * LINE_WORDS + slot, sn);
 }
 template <typename T>
 __device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,

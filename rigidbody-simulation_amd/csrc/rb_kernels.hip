@@ -440,7 +440,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // next step's broadphase: the slot atomic goes first (a later load or
     // atomic would wait for every older store), its round trip overlaps the
     // snapshot store and the quaternion update
-    Claim cl{0u, -1};
+    Claim cl{0u, 0, 0ull, 0u};
     if (p.next.line) cl = claim_slot(p.grid, p.next, p.err, sn, gen_next);
     wt_store(p.snap_next + i, sn);
     if (p.bounds) {                              // halo exchange: this body's new cell
