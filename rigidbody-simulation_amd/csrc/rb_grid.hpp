@@ -124,6 +124,32 @@ __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz
     return bucket_hash(ix, iy, iz) & g.hmask;
 }
 
+// The buckets of a body's 2x2x2 neighbourhood (cells cx + {0, sx}, cy +
+// {0, sy}, cz + {0, sz}; bit k of the index picks the neighbour along x, y,
+// z).  Under the linear group layout a bucket is a sum of one term per axis,
+// so the eight are six terms and eight sums; otherwise bucket_of each.
+template <typename T>
+__device__ __forceinline__ void neighbour_buckets(const Grid<T> &g, int32_t cx, int32_t cy, int32_t cz, int32_t sx,
+                                                  int32_t sy, int32_t sz, uint32_t (&b)[8]) {
+    if (g.super >> 24) {
+        const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
+        const int lx = (g.super >> 12) & 15, ly = (g.super >> 16) & 15, lz = (g.super >> 20) & 15;
+        // term(c) = group bits << (gb + group offset) | in-group bits << in-group offset
+        auto term = [](int32_t c, int bc, int lc, int goff, int ioff) {
+            return ((((uint32_t)(c >> bc)) & ((1u << lc) - 1u)) << goff) | (((uint32_t)c & ((1u << bc) - 1u)) << ioff);
+        };
+        const uint32_t x0 = term(cx, bx, lx, gb, 0), x1 = term(cx + sx, bx, lx, gb, 0);
+        const uint32_t y0 = term(cy, by, ly, gb + lx, bx), y1 = term(cy + sy, by, ly, gb + lx, bx);
+        const uint32_t z0 = term(cz, bz, lz, gb + lx + ly, bx + by), z1 = term(cz + sz, bz, lz, gb + lx + ly, bx + by);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = ((k & 1) ? x1 : x0) | ((k & 2) ? y1 : y0) | ((k & 4) ? z1 : z0);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), g);
+}
+
 // cell coordinates; false for non-finite / out-of-range positions
 template <typename T>
 __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, int32_t &iy, int32_t &iz) {
@@ -244,9 +270,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     uint32_t b[8];
     int32_t c[8];
     uint4 hd[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid);
+    neighbour_buckets(p.grid, cx, cy, cz, sx, sy, sz, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         if (RB_ABLATE == 6 && (k & 4) && cz + sz < 0) hd[k] = uint4{0u, 0u, 0u, 0u};
@@ -382,11 +406,13 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     uint32_t b[8];
     int32_t c[8];
     Head6 hd[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        b[k] = bucket_of(cx + ((k & 1) ? sx : 0), cy + ((k & 2) ? sy : 0), cz + ((k & 4) ? sz : 0), p.grid);
+    neighbour_buckets(p.grid, cx, cy, cz, sx, sy, sz, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) hd[k] = bucket_head6(p.cur, (uint32_t)CHK(b[k], p.grid.H));
+    // the head loads issue here, before the body work: left to itself the
+    // scheduler hoisted the work (and its waits for the state loads) above
+    // them, and the head round trip started only after it
+    __builtin_amdgcn_sched_barrier(0);
     overlap();                                    // body work under the head loads
     STAMP(8);
     int32_t n = 0;

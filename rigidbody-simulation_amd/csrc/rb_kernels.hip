@@ -192,6 +192,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     Snap<T> p4[QS];
 #pragma unroll
     for (int u = 0; u < QS; ++u) p4[u] = p.cur.pos[base + u];
+    __builtin_amdgcn_sched_barrier(0);            // the bucket loads issue before the body work
     overlap();                                    // body work under the bucket loads
     int32_t c = !ok ? 0 : head_count(id4, gen);
     STAMP(9);
