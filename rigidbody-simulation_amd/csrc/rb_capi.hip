@@ -719,25 +719,34 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // 6 % faster at 65k bodies (flat), 5 % (incline), 12 % at 1M; hashed
     // groups were bimodal (a group collision doubles the bodies of every
     // bucket in both groups and sends waves through the wide form's extra
-    // round trip for buckets of 7+ ids).  The cooperative form
-    // keeps a hash per cell.  RBHIP_HASH_GROUP=bx:by:bz (hashed groups of
-    // 2^bx x 2^by x 2^bz cells) or bx:by:bz:l (linear) overrides.
-    w->group = coop_world ? 0 : 0x233;
+    // round trip for buckets of 7+ ids).  Those kernels compute
+    // the linear layout directly (rb_grid.hpp LAYOUT_LINEAR), so their worlds
+    // always use it.  The cooperative form keeps a hash per cell.
+    // RBHIP_HASH_GROUP=bx:by:bz sets the group shape (2^bx x 2^by x 2^bz
+    // cells); in cooperative worlds bx:by:bz hashes the groups and
+    // bx:by:bz:l lays them out linearly.
+    int gshape = coop_world ? 0 : 0x233;
     bool linear = !coop_world;
     if (const char *ev = getenv("RBHIP_HASH_GROUP")) {
         int bx = 0, by = 0, bz = 0;
         char mode = 'h';
         if (sscanf(ev, "%d:%d:%d:%c", &bx, &by, &bz, &mode) >= 3 && bx >= 0 && by >= 0 && bz >= 0 && bx + by + bz <= 12)
-            w->group = bx | (by << 4) | (bz << 8);
-        linear = mode == 'l';      // bx:by:bz hashed, bx:by:bz:l linear
+            gshape = bx | (by << 4) | (bz << 8);
+        if (coop_world) linear = mode == 'l';
     }
-    while (w->group && (int64_t(1) << ((w->group & 15) + ((w->group >> 4) & 15) + ((w->group >> 8) & 15))) > w->H / 4)
-        w->group = 0;              // a table too small for the groups: one hash per cell
-    if (w->group && linear) {
+    auto gbits = [](int g) { return (g & 15) + ((g >> 4) & 15) + ((g >> 8) & 15); };
+    // a table too small for the groups: smaller groups (linear), none (hashed)
+    while (gshape && (int64_t(1) << gbits(gshape)) > w->H / 4) {
+        if (!linear) { gshape = 0; break; }
+        for (int sh = 8; sh >= 0; sh -= 4)
+            if ((gshape >> sh) & 15) { gshape -= 1 << sh; break; }
+    }
+    w->group = gshape;
+    if (linear) {
         // the group slots split into a period of 2^lx x 2^ly x 2^lz groups (z: at most 8)
         int lg = 0;
         while ((int64_t(1) << (lg + 1)) <= w->H) ++lg;
-        lg -= (w->group & 15) + ((w->group >> 4) & 15) + ((w->group >> 8) & 15);
+        lg -= gbits(gshape);
         const int lz = lg / 3 < 3 ? lg / 3 : 3, lx = (lg - lz + 1) / 2, ly = lg - lz - lx;
         w->group |= (lx << 12) | (ly << 16) | (lz << 20) | (1 << 24);
     }

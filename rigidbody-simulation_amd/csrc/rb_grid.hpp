@@ -103,8 +103,24 @@ __device__ __forceinline__ uint32_t bucket_hash(int32_t ix, int32_t iy, int32_t 
 // share buckets (hashed groups of a compact scene collide with a birthday
 // probability near 1, and a collision doubles the bodies of every bucket in
 // both groups).
+// the linear group layout (Grid::super bit 24)
 template <typename T>
+__device__ __forceinline__ uint32_t bucket_linear(int32_t ix, int32_t iy, int32_t iz, const Grid<T> &g) {
+    const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
+    const int lx = (g.super >> 12) & 15, ly = (g.super >> 16) & 15, lz = (g.super >> 20) & 15;
+    const uint32_t sc = ((uint32_t)(ix >> bx) & ((1u << lx) - 1u)) | (((uint32_t)(iy >> by) & ((1u << ly) - 1u)) << lx) |
+                        (((uint32_t)(iz >> bz) & ((1u << lz) - 1u)) << (lx + ly));
+    const uint32_t in = (uint32_t)(ix & ((1 << bx) - 1)) | ((uint32_t)(iy & ((1 << by) - 1)) << bx) |
+                        ((uint32_t)(iz & ((1 << bz) - 1)) << (bx + by));
+    return (sc << gb) | in;
+}
+// Layouts a kernel may assume at compile time: LAYOUT_LINEAR in the one-lane
+// and wide forms (their worlds always use it: rb_capi.hip), LAYOUT_ANY
+// reads Grid::super
+enum : int { LAYOUT_ANY = 0, LAYOUT_LINEAR = 1 };
+template <int L = LAYOUT_ANY, typename T>
 __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, const Grid<T> &g) {
+    if (L == LAYOUT_LINEAR) return bucket_linear(ix, iy, iz, g);
     if (g.super) {
         const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
         // arithmetic shifts: floor(c / 2^b)
@@ -128,10 +144,10 @@ __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz
 // {0, sy}, cz + {0, sz}; bit k of the index picks the neighbour along x, y,
 // z).  Under the linear group layout a bucket is a sum of one term per axis,
 // so the eight are six terms and eight sums; otherwise bucket_of each.
-template <typename T>
+template <int L = LAYOUT_ANY, typename T>
 __device__ __forceinline__ void neighbour_buckets(const Grid<T> &g, int32_t cx, int32_t cy, int32_t cz, int32_t sx,
                                                   int32_t sy, int32_t sz, uint32_t (&b)[8]) {
-    if (g.super >> 24) {
+    if (L == LAYOUT_LINEAR || (g.super >> 24)) {
         const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
         const int lx = (g.super >> 12) & 15, ly = (g.super >> 16) & 15, lz = (g.super >> 20) & 15;
         // term(c) = group bits << (gb + group offset) | in-group bits << in-group offset
@@ -177,13 +193,13 @@ struct Claim {
     unsigned long long old;      // the header before this claim (valid if ok)
     uint32_t gen;
 };
-template <typename T>
+template <int L = LAYOUT_ANY, typename T>
 __device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
                                             uint32_t gen) {
     int32_t ix = 0, iy = 0, iz = 0;
     const bool in = cell_of(sn.x, sn.y, sn.z, g.inv_cs, ix, iy, iz);
     if (!in) atomicOr(err, ERR_DOMAIN);
-    const uint32_t b = bucket_of(ix, iy, iz, g);
+    const uint32_t b = bucket_of<L>(ix, iy, iz, g);
     // no defined value when !in (never decoded then): a constant here would
     // make the join select it against the atomic's return, i.e. wait for it
     unsigned long long old = __builtin_nondeterministic_value(0ull);
@@ -261,7 +277,7 @@ __device__ __forceinline__ void list_insert(int32_t *s_id, int stride, int slot,
 // loads in flight together); hit(tagged id, snapshot) decides a partner.
 // The partners go to the body's LDS column of s_id in ascending id order.
 // Returns the partner count.
-template <typename T, int MAXP, typename Hit>
+template <typename T, int MAXP, int L = LAYOUT_ANY, typename Hit>
 __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
                                                   int tid, uint32_t gen, Hit hit) {
     constexpr int NB = STEP_BLOCK;
@@ -270,7 +286,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     uint32_t b[8];
     int32_t c[8];
     uint4 hd[8];
-    neighbour_buckets(p.grid, cx, cy, cz, sx, sy, sz, b);
+    neighbour_buckets<L>(p.grid, cx, cy, cz, sx, sy, sz, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         if (RB_ABLATE == 6 && (k & 4) && cz + sz < 0) hd[k] = uint4{0u, 0u, 0u, 0u};
@@ -406,7 +422,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     uint32_t b[8];
     int32_t c[8];
     Head6 hd[8];
-    neighbour_buckets(p.grid, cx, cy, cz, sx, sy, sz, b);
+    neighbour_buckets<LAYOUT_LINEAR>(p.grid, cx, cy, cz, sx, sy, sz, b);
 #pragma unroll
     for (int k = 0; k < 8; ++k) hd[k] = bucket_head6(p.cur, (uint32_t)CHK(b[k], p.grid.H));
     // the head loads issue here, before the body work: left to itself the

@@ -140,7 +140,9 @@ __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i,
 template <typename T, int MAXP, bool BOXES>
 __device__ __forceinline__ int32_t search_partners(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                    T rad, T bi, int32_t *s_id, int tid, uint32_t gen, bool &defer) {
-    return search_buckets<T, MAXP>(p, i, x, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
+    // the box kernel also runs in cooperative worlds (a hash per cell)
+    constexpr int L = BOXES ? LAYOUT_ANY : LAYOUT_LINEAR;
+    return search_buckets<T, MAXP, L>(p, i, x, s_id, tid, gen, [&](uint32_t tj, const Snap<T> &s) {
         return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s, defer);
     });
 }
@@ -442,7 +444,11 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // atomic would wait for every older store), its round trip overlaps the
     // snapshot store and the quaternion update
     Claim cl{0u, 0, 0ull, 0u};
-    if (p.next.line) cl = claim_slot(p.grid, p.next, p.err, sn, gen_next);
+    // the one-lane and wide forms (and the split form's update) run in
+    // linear-layout worlds only; the cooperative form and the box kernel
+    // read the layout
+    constexpr int L = (PM == 2 || (PM == 0 && !BOXES)) ? LAYOUT_LINEAR : LAYOUT_ANY;
+    if (p.next.line) cl = claim_slot<L>(p.grid, p.next, p.err, sn, gen_next);
     wt_store(p.snap_next + i, sn);
     if (p.bounds) {                              // halo exchange: this body's new cell
         int32_t cx, cy, cz;
