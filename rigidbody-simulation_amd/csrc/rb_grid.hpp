@@ -441,10 +441,13 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
             if (b[j] == b[k]) m = 0;                  // two cells hashed to one bucket: visit once
         c[k] = m;
         more |= m > WIDE_HEAD_IDS;
+        // branch-free: every id is written at the list's end, which advances
+        // only for a listed one (the last write lands at index <= WIDE_MAXC-1)
 #define RB_WIDE_LIST(S)                                                           \
-        if (S < m) {                                                              \
+        {                                                                         \
             const uint32_t t = head6_id<S>(hd[k]);                                \
-            if ((t & ~BOX_FLAG) != (uint32_t)i) s_cand[n++ * NB + tid] = t;       \
+            s_cand[n * NB + tid] = t;                                             \
+            n += (S < m && (t & ~BOX_FLAG) != (uint32_t)i) ? 1 : 0;               \
         }
         RB_WIDE_LIST(0) RB_WIDE_LIST(1) RB_WIDE_LIST(2) RB_WIDE_LIST(3) RB_WIDE_LIST(4) RB_WIDE_LIST(5)
 #undef RB_WIDE_LIST

@@ -279,15 +279,32 @@ template <typename T> struct BodyIn {
     T m;
     V3<T> I;
 };
-template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepParams<T> &p, int32_t l, int32_t i) {
+template <typename T>
+__device__ __forceinline__ BodyIn<T> load_body(const BodyState<T> &st, const BodyConsts<T> &cs, int32_t l, int32_t i) {
     BodyIn<T> b;
-    b.q = {p.st.qw()[l], p.st.qx()[l], p.st.qy()[l], p.st.qz()[l]};
-    b.v = {p.st.vx()[l], p.st.vy()[l], p.st.vz()[l]};
-    b.w = {p.st.wx()[l], p.st.wy()[l], p.st.wz()[l]};
-    b.m = p.cs.mass()[i];
-    b.I = {p.cs.ix()[i], p.cs.iy()[i], p.cs.iz()[i]};
+    b.q = {st.qw()[l], st.qx()[l], st.qy()[l], st.qz()[l]};
+    b.v = {st.vx()[l], st.vy()[l], st.vz()[l]};
+    b.w = {st.wx()[l], st.wy()[l], st.wz()[l]};
+    b.m = cs.mass()[i];
+    b.I = {cs.ix()[i], cs.iy()[i], cs.iz()[i]};
     return b;
 }
+template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepParams<T> &p, int32_t l, int32_t i) {
+    return load_body(p.st, p.cs, l, i);
+}
+
+// The fields a step's first loads need (the body's snapshot, kind, state and
+// constants).  The wide kernel takes them as leading scalar arguments, which
+// gfx950 preloads into SGPRs as its waves launch (the wide unit is built with
+// -amdgpu-kernarg-preload-count), so its first loads wait for no scalar load
+// of the parameter block; the other kernels take them from it.
+template <typename T> struct Lead {
+    const Snap<T> *snap_cur;
+    BodyState<T> st;
+    BodyConsts<T> cs;
+    int32_t n_local, lo;
+    __device__ static Lead of(const StepParams<T> &p) { return Lead{p.snap_cur, p.st, p.cs, p.n_local, p.lo}; }
+};
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 template <typename T>
@@ -479,23 +496,24 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 // one-lane form for one wave per SIMD (search_buckets_wide; state loads and
 // inv(I_w) under the head loads).
 template <typename T, int MAXP, int G, bool WIDE, bool BOXES>
-__device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, int64_t lb, int slot, int k, int tid,
+__device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> &ld, bool active, int64_t lb, int slot,
+                                          int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
                                           uint32_t *s_cand, int32_t *cell, uint32_t gen, T *s_poly,
                                           uint8_t *s_didx = nullptr, Snap<T> *s_hpos = nullptr) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
-    const int32_t i = p.lo + l;
+    const int32_t i = ld.lo + l;
 
     // ---- K1 first: the contact search reads only step-start data -----------
-    const Snap<T> self = p.snap_cur[i];
+    const Snap<T> self = ld.snap_cur[i];
     const V3<T> x = {self.x, self.y, self.z};
-    const int32_t kind = p.cs.kind[i];
+    const int32_t kind = ld.cs.kind[i];
     const T bi = self.r;
     // half extents y, z only matter for boxes; loaded for every body (a load
     // under a kind test would wait for kind before the state loads issue)
-    const T sy = p.cs.sy()[i], szz = p.cs.sz()[i];
-    const V3<T> sz = {p.cs.sx()[i], kind != 0 ? sy : T(0), kind != 0 ? szz : T(0)};
+    const T sy = ld.cs.sy()[i], szz = ld.cs.sz()[i];
+    const V3<T> sz = {ld.cs.sx()[i], kind != 0 ? sy : T(0), kind != 0 ? szz : T(0)};
     BodyIn<T> in;
     LazyInvI<T> invI;
     bool forced = false;
@@ -503,9 +521,16 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, bool active, i
     // with them issued after the bucket heads, C3)
     constexpr bool early = G > 1 || WIDE;
     if constexpr (early) {
-        in = load_body(p, l, i);
+        in = load_body(ld.st, ld.cs, l, i);
         invI.I = in.I;
         invI.q = in.q;
+    }
+    if constexpr (WIDE) {
+        // the parameter block's fields the search starts with, in one scalar
+        // round trip under the body's loads (which needed none of them)
+        asm volatile("" ::"s"(p.grid.inv_cs), "s"(p.grid.H), "s"(p.grid.super), "s"(p.cur.line), "s"(p.cur.gen),
+                     "s"(p.n_global), "s"(p.xfrc));
+        gen = *p.cur.gen;
     }
     STAMP(1);
     int32_t np_ = 0;
@@ -577,7 +602,7 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
 }
 
 template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false>
-__device__ __forceinline__ void step_body(const StepParams<T> &p) {
+__device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> &ld) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
     __shared__ T s_poly[BOXES ? 48 * NB : 1];   // box-box face clipping: 2 x 8 vertices x 3 per body
@@ -603,8 +628,12 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     // their own, each after a wait for the one before, they held the
     // own-snapshot loads back two more scalar round trips in the one-lane
     // forms)
-    asm volatile("" ::"s"(p.snap_cur), "s"(p.st.base), "s"(p.st.S), "s"(p.cs.base), "s"(p.cs.Npad), "s"(p.cs.kind),
-                 "s"(p.n_local), "s"(p.lo), "s"(p.cur.gen), "s"(p.next.line), "s"(p.next.gen), "s"(p.epoch));
+    // (the wide kernel's lead fields are preloaded: its parameter block's
+    // loads are waited for only under the body's first loads, body_step)
+    if constexpr (!WIDE)
+        asm volatile("" ::"s"(ld.snap_cur), "s"(ld.st.base), "s"(ld.st.S), "s"(ld.cs.base), "s"(ld.cs.Npad),
+                     "s"(ld.cs.kind), "s"(ld.n_local), "s"(ld.lo), "s"(p.cur.gen), "s"(p.next.line), "s"(p.next.gen),
+                     "s"(p.epoch));
 
     // Block 0 advances the exchange's step number and publishes the next
     // table's generation (one more than the one this step reads) for the
@@ -612,21 +641,21 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
     // the end: a store ahead of the body loads holds them back (they may not
     // pass it), which cost its waves a scalar round trip (+11 % at 16k
     // bodies).  The one-lane forms measured no gain (65k) or a loss (1M).
-    constexpr bool late_publish = G > 1;
+    constexpr bool late_publish = G > 1 || WIDE;
     if (!late_publish && p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;
-    const uint32_t gen = *p.cur.gen;
+    const uint32_t gen = WIDE ? 0u : *p.cur.gen;    // the wide form loads it in body_step
     if (!late_publish && p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
 
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
-    const bool active = lb < p.n_local;
+    const bool active = lb < ld.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
     if (G > 1 || active)
-        body_step<T, MAXP, G, WIDE, BOXES>(p, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen,
+        body_step<T, MAXP, G, WIDE, BOXES>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen,
                                            s_poly, s_didx, s_hpos);
     if (p.bounds) fold_bounds(p.bounds, cell);
     if (late_publish && blockIdx.x == 0 && tid == 0) {
-        if (p.next.line) *p.next.gen = gen + 1u;
+        if (p.next.line) *p.next.gen = (WIDE ? *p.cur.gen : gen) + 1u;
         if (p.epoch) *p.epoch += 1;
     }
 }
@@ -645,13 +674,13 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p) {
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(MAXP <= 16 ? RB_MIN_WAVES_COOP : 2)))   // 32 partners: 2 fit
-void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8, false, false>(p); }
+void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8, false, false>(p, Lead<T>::of(p)); }
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
 #if RB_MIN_WAVES_G1 > 1
 __attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_G1)))
 #endif
-void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1, false, false>(p); }
+void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1, false, false>(p, Lead<T>::of(p)); }
 // The box kernel (box worlds, after the step kernel): steps the bodies the
 // step kernel deferred — those with a box-involved partner within bounding
 // range — one lane per body with the box narrowphase (rb_boxes.hpp), from
@@ -669,7 +698,7 @@ void box_kernel(StepParams<T> p) {
     for (int64_t qi = (int64_t)blockIdx.x * STEP_BLOCK + tid; qi < n; qi += (int64_t)gridDim.x * STEP_BLOCK) {
         int32_t cell[3] = {INT32_MAX, 0, 0};
         // one lane per body: the lane's LDS column (partner list, polygon) is slot = tid
-        body_step<T, MAXP, 1, false, true>(p, true, p.defer_q[qi], tid, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
+        body_step<T, MAXP, 1, false, true>(p, Lead<T>::of(p), true, p.defer_q[qi], tid, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
                                            cell, gen, s_poly);
     }
     if (blockIdx.x == 0 && tid == 0) *p.defer_reset = 0;    // the next step's queue
@@ -677,7 +706,11 @@ void box_kernel(StepParams<T> p) {
 // one wave per SIMD (up to 64 x 1024 owned bodies): every register is free
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void step_kernel_wide(StepParams<T> p) { step_body<T, MAXP, 1, true, false>(p); }
+void step_kernel_wide(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
+                      const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
+    step_body<T, MAXP, 1, true, false>(
+        p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
+}
 
 // ---- split form (large scenes): search kernel + update kernel -------------
 // The fused kernel's register footprint (the f64 solve) caps it at two
@@ -900,8 +933,13 @@ template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, 
 template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, hipStream_t s) {
     int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
     if (blocks < 1) blocks = 1;
-    if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-    else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    // the lead fields as separate scalar arguments: preloaded (step_kernel_wide)
+    if (maxp <= 16)
+        hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p.snap_cur, p.st.base,
+                           p.st.S, p.cs.base, p.cs.Npad, p.cs.kind, p.n_local, p.lo, p);
+    else
+        hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p.snap_cur, p.st.base,
+                           p.st.S, p.cs.base, p.cs.Npad, p.cs.kind, p.n_local, p.lo, p);
     return hipGetLastError();
 }
 
