@@ -294,10 +294,11 @@ template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepP
 }
 
 // The fields a step's first loads need (the body's snapshot, kind, state and
-// constants).  The wide kernel takes them as leading scalar arguments, which
-// gfx950 preloads into SGPRs as its waves launch (the wide unit is built with
-// -amdgpu-kernarg-preload-count), so its first loads wait for no scalar load
-// of the parameter block; the other kernels take them from it.
+// constants).  The step kernels take them as leading scalar arguments, which
+// gfx950 preloads into SGPRs as the waves launch (the units are built with
+// -amdgpu-kernarg-preload-count), so their first loads wait for no scalar
+// load of the parameter block (measured 0.27 us per launch in
+// scripts/preload_probe.hip); the box kernel takes them from the block.
 template <typename T> struct Lead {
     const Snap<T> *snap_cur;
     BodyState<T> st;
@@ -305,6 +306,7 @@ template <typename T> struct Lead {
     int32_t n_local, lo;
     __device__ static Lead of(const StepParams<T> &p) { return Lead{p.snap_cur, p.st, p.cs, p.n_local, p.lo}; }
 };
+#define LEAD_ARGS(p) (p).snap_cur, (p).st.base, (p).st.S, (p).cs.base, (p).cs.Npad, (p).cs.kind, (p).n_local, (p).lo
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 template <typename T>
@@ -495,7 +497,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 // One body (G lanes): contact search, then (lane 0) the update.  WIDE: the
 // one-lane form for one wave per SIMD (search_buckets_wide; state loads and
 // inv(I_w) under the head loads).
-template <typename T, int MAXP, int G, bool WIDE, bool BOXES>
+template <typename T, int MAXP, int G, bool WIDE, bool BOXES, bool PRE = false>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> &ld, bool active, int64_t lb, int slot,
                                           int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
@@ -525,11 +527,13 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
         invI.I = in.I;
         invI.q = in.q;
     }
-    if constexpr (WIDE) {
-        // the parameter block's fields the search starts with, in one scalar
-        // round trip under the body's loads (which needed none of them)
+    if constexpr (PRE) {
+        // preloaded lead (step_body): the parameter block's fields the search
+        // starts with, in one scalar round trip under the body's loads (which
+        // needed none of them)
         asm volatile("" ::"s"(p.grid.inv_cs), "s"(p.grid.H), "s"(p.grid.super), "s"(p.cur.line), "s"(p.cur.gen),
                      "s"(p.n_global), "s"(p.xfrc));
+        if constexpr (G > 1) asm volatile("" ::"s"(p.cur.pos));
         gen = *p.cur.gen;
     }
     STAMP(1);
@@ -622,40 +626,23 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
         rb_stamp_buf[blockIdx.x][14] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
     }
 #endif
-    // one scalar round trip for the prologue's kernel arguments (the
-    // scheduler would otherwise issue the second load after the first wait)
-    // (the table generations' addresses and the next table's too: loaded on
-    // their own, each after a wait for the one before, they held the
-    // own-snapshot loads back two more scalar round trips in the one-lane
-    // forms)
-    // (the wide kernel's lead fields are preloaded: its parameter block's
-    // loads are waited for only under the body's first loads, body_step)
-    if constexpr (!WIDE)
-        asm volatile("" ::"s"(ld.snap_cur), "s"(ld.st.base), "s"(ld.st.S), "s"(ld.cs.base), "s"(ld.cs.Npad),
-                     "s"(ld.cs.kind), "s"(ld.n_local), "s"(ld.lo), "s"(p.cur.gen), "s"(p.next.line), "s"(p.next.gen),
-                     "s"(p.epoch));
-
+    // The lead (the body's first loads' fields) is preloaded; body_step waits
+    // for the parameter block's scalar loads only under the body's loads.
     // Block 0 advances the exchange's step number and publishes the next
     // table's generation (one more than the one this step reads) for the
-    // kernels that insert after this one.  The cooperative form does it at
-    // the end: a store ahead of the body loads holds them back (they may not
-    // pass it), which cost its waves a scalar round trip (+11 % at 16k
-    // bodies).  The one-lane forms measured no gain (65k) or a loss (1M).
-    constexpr bool late_publish = G > 1 || WIDE;
-    if (!late_publish && p.epoch && blockIdx.x == 0 && tid == 0) *p.epoch += 1;
-    const uint32_t gen = WIDE ? 0u : *p.cur.gen;    // the wide form loads it in body_step
-    if (!late_publish && p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen + 1u;
+    // kernels that insert after this one, at the end: a store ahead of the
+    // body loads would hold them back (they may not pass it).
 
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < ld.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
     if (G > 1 || active)
-        body_step<T, MAXP, G, WIDE, BOXES>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell, gen,
-                                           s_poly, s_didx, s_hpos);
+        body_step<T, MAXP, G, WIDE, BOXES, true>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell,
+                                                 0u /* loaded in body_step */, s_poly, s_didx, s_hpos);
     if (p.bounds) fold_bounds(p.bounds, cell);
-    if (late_publish && blockIdx.x == 0 && tid == 0) {
-        if (p.next.line) *p.next.gen = (WIDE ? *p.cur.gen : gen) + 1u;
+    if (blockIdx.x == 0 && tid == 0) {
+        if (p.next.line) *p.next.gen = *p.cur.gen + 1u;
         if (p.epoch) *p.epoch += 1;
     }
 }
@@ -674,13 +661,21 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(MAXP <= 16 ? RB_MIN_WAVES_COOP : 2)))   // 32 partners: 2 fit
-void step_kernel_coop(StepParams<T> p) { step_body<T, MAXP, 8, false, false>(p, Lead<T>::of(p)); }
+void step_kernel_coop(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
+                      const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
+    step_body<T, MAXP, 8, false, false>(
+        p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
+}
 template <typename T, int MAXP>
 __global__ __launch_bounds__(STEP_BLOCK)
 #if RB_MIN_WAVES_G1 > 1
 __attribute__((amdgpu_waves_per_eu(RB_MIN_WAVES_G1)))
 #endif
-void step_kernel_one(StepParams<T> p) { step_body<T, MAXP, 1, false, false>(p, Lead<T>::of(p)); }
+void step_kernel_one(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
+                     const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
+    step_body<T, MAXP, 1, false, false>(
+        p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
+}
 // The box kernel (box worlds, after the step kernel): steps the bodies the
 // step kernel deferred — those with a box-involved partner within bounding
 // range — one lane per body with the box narrowphase (rb_boxes.hpp), from
@@ -881,14 +876,14 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
         else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
     } else if (coop) {
-        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+        else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     } else if (form == FORM_WIDE) {
         const hipError_t we = launch_step_wide<T>(p, maxp, s);
         if (we != hipSuccess) return we;
     } else {
-        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((step_kernel_one<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+        else hipLaunchKernelGGL((step_kernel_one<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     }
     if (boxes) {
         const int64_t bb = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
@@ -933,13 +928,8 @@ template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, 
 template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, hipStream_t s) {
     int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
     if (blocks < 1) blocks = 1;
-    // the lead fields as separate scalar arguments: preloaded (step_kernel_wide)
-    if (maxp <= 16)
-        hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p.snap_cur, p.st.base,
-                           p.st.S, p.cs.base, p.cs.Npad, p.cs.kind, p.n_local, p.lo, p);
-    else
-        hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p.snap_cur, p.st.base,
-                           p.st.S, p.cs.base, p.cs.Npad, p.cs.kind, p.n_local, p.lo, p);
+    if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+    else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     return hipGetLastError();
 }
 
