@@ -169,7 +169,7 @@ __device__ __forceinline__ void ball_body(const StepParams<T> &p, int32_t l, int
     ball_ground(p, x, v, w, mi, ri, Ii);
     Snap<T> sn;
     sn.x = x.x; sn.y = x.y; sn.z = x.z; sn.r = ri;
-    Claim cl{0u, 0, 0ull, 0u};
+    Claim cl{0u, 0, 0ull, 0u, 0};
     if (p.next.line) cl = claim_slot(p.grid, p.next, p.err, sn, gen + 1u);
     wt_store(p.snap_next + i, sn);
     Vel<T> vn;

@@ -107,7 +107,7 @@ struct rb_world {
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
-    uint32_t *ids[2] = {};     // [H][LINE_WORDS] bucket lines: header + ids (alternate with the snapshots)
+    uint32_t *ids[2] = {};     // [H][LINE_WORDS] bucket blocks (rb_internal.hpp Table; alternate with the snapshots)
     void *pos[2] = {};         // [H][LINE_WORDS] Snap<T> bucket slot snapshots
     uint32_t *gen = nullptr;   // [2] generation of the table of each step parity (rb_internal.hpp Table)
     uint32_t gen_off = 1;      // generation of step c's table = gen_off + c (host bookkeeping; only grows)
@@ -750,6 +750,19 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         const int lz = lg / 3 < 3 ? lg / 3 : 3, lx = (lg - lz + 1) / 2, ly = lg - lz - lx;
         w->group |= (lx << 12) | (ly << 16) | (lz << 20) | (1 << 24);
     }
+    // heads per 128-byte line (rb_internal.hpp Table): 4 in wide-form worlds
+    // (C3 17.4 -> 16.4 us), 2 in one-lane worlds (1M 0.237 -> 0.225 ms; 4
+    // there cost 10 % at 262k), 1 in cooperative worlds (no gain measured).
+    // The cooperative and wide kernels assume theirs at compile time;
+    // RBHIP_HEADS_PER_LINE = 1, 2 or 4 sets the one-lane worlds'.
+    const bool wide_world = !coop_world && w->n_local <= w->wide_max;
+    int rl = coop_world ? 0 : wide_world ? 2 : 1;
+    if (const char *ev = getenv("RBHIP_HEADS_PER_LINE"))
+        if (!coop_world && !wide_world) {
+            const int r = atoi(ev);
+            if (r == 1 || r == 2 || r == 4) rl = r == 1 ? 0 : r == 2 ? 1 : 2;
+        }
+    w->group |= rl << 25;
     int64_t nsph = 0;
     for (int64_t b = 0; b < w->N; ++b) nsph += d->kind[b] == RB_BODY_SPHERE;
     // algorithmic bytes per body-step: 13 state reals read + 13

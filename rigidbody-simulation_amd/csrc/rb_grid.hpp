@@ -121,12 +121,12 @@ enum : int { LAYOUT_ANY = 0, LAYOUT_LINEAR = 1 };
 template <int L = LAYOUT_ANY, typename T>
 __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz, const Grid<T> &g) {
     if (L == LAYOUT_LINEAR) return bucket_linear(ix, iy, iz, g);
-    if (g.super) {
+    if (g.super & 0x1ffffff) {                 // (bits 25-26: heads per line, not the layout)
         const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
         // arithmetic shifts: floor(c / 2^b)
         const int32_t gx = ix >> bx, gy = iy >> by, gz = iz >> bz;
         uint32_t sc;
-        if (g.super >> 24) {
+        if ((g.super >> 24) & 1) {
             const int lx = (g.super >> 12) & 15, ly = (g.super >> 16) & 15, lz = (g.super >> 20) & 15;
             sc = ((uint32_t)gx & ((1u << lx) - 1u)) | (((uint32_t)gy & ((1u << ly) - 1u)) << lx) |
                  (((uint32_t)gz & ((1u << lz) - 1u)) << (lx + ly));
@@ -147,7 +147,7 @@ __device__ __forceinline__ uint32_t bucket_of(int32_t ix, int32_t iy, int32_t iz
 template <int L = LAYOUT_ANY, typename T>
 __device__ __forceinline__ void neighbour_buckets(const Grid<T> &g, int32_t cx, int32_t cy, int32_t cz, int32_t sx,
                                                   int32_t sy, int32_t sz, uint32_t (&b)[8]) {
-    if (L == LAYOUT_LINEAR || (g.super >> 24)) {
+    if (L == LAYOUT_LINEAR || ((g.super >> 24) & 1)) {
         const int bx = g.super & 15, by = (g.super >> 4) & 15, bz = (g.super >> 8) & 15, gb = bx + by + bz;
         const int lx = (g.super >> 12) & 15, ly = (g.super >> 16) & 15, lz = (g.super >> 20) & 15;
         // term(c) = group bits << (gb + group offset) | in-group bits << in-group offset
@@ -187,13 +187,34 @@ __device__ __forceinline__ bool cell_of(T x, T y, T z, T inv_cs, int32_t &ix, in
 // publish_slot: decoding it in claim_slot, at the join of the caller's
 // branches around the claim, made the compiler wait for the atomic right
 // there, ahead of all the work placed between the two.
+// Bucket b's head (header, then its first ids) and the word of its slot s,
+// in blocks of R = 2^rl buckets (rb_internal.hpp Table): the block's first
+// line holds the R heads of 32/R words, its other lines the further ids.
+__device__ __forceinline__ int grid_rl(int32_t super) { return (super >> 25) & 3; }
+__device__ __forceinline__ int64_t head_offset(uint32_t b, int rl) {
+    return ((int64_t)(b >> rl) << (5 + rl)) + (int64_t)(b & ((1u << rl) - 1u)) * (LINE_WORDS >> rl);
+}
+template <typename T> __device__ __forceinline__ uint32_t *head_words(const Table<T> &tab, uint32_t b, int rl) {
+    return tab.line + head_offset((uint32_t)CHK(b, RB_BOUNDS ? 1ll << 40 : 0), rl);
+}
+template <typename T> __device__ __forceinline__ uint32_t *slot_word(const Table<T> &tab, uint32_t b, int s, int rl) {
+    if (rl == 0) return tab.line + (int64_t)b * LINE_WORDS + HEAD_WORDS + s;    // one bucket per line
+    const int hw = LINE_WORDS >> rl, hid = hw - HEAD_WORDS;         // head words, ids in the head
+    const uint32_t r = b & ((1u << rl) - 1u);
+    const int64_t blk = (int64_t)(b >> rl) << (5 + rl);
+    return tab.line + (s < hid ? blk + (int64_t)r * hw + HEAD_WORDS + s
+                               : blk + LINE_WORDS + (int64_t)r * (LINE_WORDS - hw) + (s - hid));
+}
+
 struct Claim {
     uint32_t b;
     int32_t ok;                  // 0: not inserted (no table, or a non-finite position)
     unsigned long long old;      // the header before this claim (valid if ok)
     uint32_t gen;
+    int32_t rl;                  // the table's log2 heads per line
 };
-template <int L = LAYOUT_ANY, typename T>
+// RL: the table's log2 heads per line when known at compile time (-1: Grid::super)
+template <int L = LAYOUT_ANY, int RL = -1, typename T>
 __device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &tab, int32_t *err, const Snap<T> &sn,
                                             uint32_t gen) {
     int32_t ix = 0, iy = 0, iz = 0;
@@ -204,13 +225,13 @@ __device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &ta
     // make the join select it against the atomic's return, i.e. wait for it
     unsigned long long old = __builtin_nondeterministic_value(0ull);
     if (in) {
-        auto *h = reinterpret_cast<unsigned long long *>(tab.line + (int64_t)CHK(b, g.H) * LINE_WORDS);
+        auto *h = reinterpret_cast<unsigned long long *>(head_words(tab, (uint32_t)CHK(b, g.H), RL >= 0 ? RL : grid_rl(g.super)));
         atomicMax(h, (unsigned long long)gen << 32);
         old = atomicAdd(h, 1ull);
     }
-    return {b, in ? 1 : 0, old, gen};
+    return {b, in ? 1 : 0, old, gen, RL >= 0 ? RL : grid_rl(g.super)};
 }
-template <typename T>
+template <int RL = -1, typename T>
 __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
                                              uint32_t tagged_id) {
     if (!c.ok) return;
@@ -218,8 +239,7 @@ __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, 
     // table before the next step's launch)
     const int32_t slot = (uint32_t)(c.old >> 32) == c.gen ? (int32_t)(uint32_t)c.old : BUCKET_SLOTS;
     if (slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    const int64_t o = CHK((int64_t)c.b * LINE_WORDS + HEAD_WORDS + slot, RB_BOUNDS ? 1ll << 40 : 0);
-    wt_store(tab.line + o, tagged_id);
+    wt_store(slot_word(tab, c.b, slot, RL >= 0 ? RL : c.rl), tagged_id);
     if (tab.pos) wt_store(tab.pos + (int64_t)c.b * LINE_WORDS + slot, sn);
 }
 template <typename T>
@@ -231,15 +251,15 @@ __device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab,
 // A bucket's header and first two ids in one 16-byte load; count = 0 unless
 // the header carries the table's generation (clamped to the slots).
 template <typename T>
-__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b) {
-    return *reinterpret_cast<const uint4 *>(tab.line + (int64_t)CHK(b, RB_BOUNDS ? 1ll << 40 : 0) * LINE_WORDS);
+__device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int rl) {
+    return *reinterpret_cast<const uint4 *>(head_words(tab, b, rl));
 }
 __device__ __forceinline__ int32_t head_count(const uint4 &h, uint32_t gen) {
     return h.y != gen ? 0 : h.x < (uint32_t)BUCKET_SLOTS ? (int32_t)h.x : BUCKET_SLOTS;
 }
 template <typename T>
-__device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s) {
-    return s == 0 ? h.z : s == 1 ? h.w : tab.line[(int64_t)b * LINE_WORDS + HEAD_WORDS + s];
+__device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s, int rl) {
+    return s == 0 ? h.z : s == 1 ? h.w : *slot_word(tab, b, s, rl);
 }
 
 // The 2x2x2 cell neighbourhood: cell size = 2 x the largest contact reach
@@ -287,10 +307,11 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     int32_t c[8];
     uint4 hd[8];
     neighbour_buckets<L>(p.grid, cx, cy, cz, sx, sy, sz, b);
+    const int rl = grid_rl(p.grid.super);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         if (RB_ABLATE == 6 && (k & 4) && cz + sz < 0) hd[k] = uint4{0u, 0u, 0u, 0u};
-        else hd[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H));
+        else hd[k] = bucket_head(p.cur, (uint32_t)CHK(b[k], p.grid.H), rl);
     }
     STAMP(8);
     int32_t total = 0;
@@ -317,17 +338,17 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
         for (int u = 0; u < RB_QBATCH; ++u) {
             int32_t rem = base + u;
             uint32_t t = (uint32_t)i;
-            int64_t addr = -1;
+            const uint32_t *at = nullptr;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 if (rem >= 0 && rem < c[k]) {
                     if (rem == 0) t = hd[k].z;
                     else if (rem == 1) t = hd[k].w;
-                    else addr = (int64_t)b[k] * LINE_WORDS + HEAD_WORDS + rem;
+                    else at = slot_word(p.cur, b[k], rem, rl);
                 }
                 rem -= c[k];
             }
-            if (base + u < total && addr >= 0) t = p.cur.line[CHK(addr, (int64_t)p.grid.H * LINE_WORDS)];
+            if (base + u < total && at) t = *at;
             tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
         // the id-indexed snapshot: ids are spatially coherent, so a wave's
@@ -386,13 +407,13 @@ __device__ __forceinline__ void list_insert_pos(int32_t *s_id, uint8_t *s_didx, 
 
 // ---- wide one-lane search (one wave per SIMD, rb_kernels.hip step_kernel_wide)
 // A bucket head of 32 bytes: header and the first WIDE_HEAD_IDS ids.
-constexpr int WIDE_HEAD_IDS = 6;
+constexpr int WIDE_HEAD_IDS = 6;                    // (heads are at least 32 bytes: R <= 4)
 constexpr int WIDE_QBATCH = 8;                      // candidates per round trip
 constexpr int WIDE_MAXC = 8 * WIDE_HEAD_IDS;        // head candidates listed in LDS
 struct Head6 { uint4 a, b; };
 template <typename T>
-__device__ __forceinline__ Head6 bucket_head6(const Table<T> &tab, uint32_t b) {
-    const uint4 *l = reinterpret_cast<const uint4 *>(tab.line + (int64_t)CHK(b, RB_BOUNDS ? 1ll << 40 : 0) * LINE_WORDS);
+__device__ __forceinline__ Head6 bucket_head6(const Table<T> &tab, uint32_t b, int rl) {
+    const uint4 *l = reinterpret_cast<const uint4 *>(head_words(tab, b, rl));
     return Head6{l[0], l[1]};
 }
 template <int S> __device__ __forceinline__ uint32_t head6_id(const Head6 &h) {
@@ -423,8 +444,9 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     int32_t c[8];
     Head6 hd[8];
     neighbour_buckets<LAYOUT_LINEAR>(p.grid, cx, cy, cz, sx, sy, sz, b);
+    constexpr int rl = 2;                         // heads per line: wide-form worlds 4 (rb_capi.hip)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) hd[k] = bucket_head6(p.cur, (uint32_t)CHK(b[k], p.grid.H));
+    for (int k = 0; k < 8; ++k) hd[k] = bucket_head6(p.cur, (uint32_t)CHK(b[k], p.grid.H), rl);
     // the head loads issue here, before the body work: left to itself the
     // scheduler hoisted the work (and its waits for the state loads) above
     // them, and the head round trip started only after it
@@ -487,7 +509,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 Snap<T> sn[QB];
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
-                    tj[u] = s0 + u < c[k] ? p.cur.line[(int64_t)b[k] * LINE_WORDS + HEAD_WORDS + s0 + u] : (uint32_t)i;
+                    tj[u] = s0 + u < c[k] ? *slot_word(p.cur, b[k], s0 + u, rl) : (uint32_t)i;
 #pragma unroll
                 for (int u = 0; u < QB; ++u) {
                     sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};

@@ -26,8 +26,8 @@ enum : int32_t {
 // layout [P][S][4], rank r's bodies are the contiguous slice [r*S, r*S+S).
 template <typename T> struct alignas(4 * sizeof(T)) Snap { T x, y, z, r; };
 
-// Broadphase buckets: per-cell hash -> one 128-byte line holding an 8-byte
-// header and 30 body ids, and (cooperative search) slot for slot the
+// Broadphase buckets: per-cell hash -> one bucket of 128 bytes holding an
+// 8-byte header and 30 body ids (laid out in blocks: below), and (cooperative search) slot for slot the
 // bodies' snapshots, so a query reads candidates' positions from the bucket
 // it already holds instead of chasing ids into the id-indexed snapshot.
 //
@@ -41,12 +41,19 @@ template <typename T> struct alignas(4 * sizeof(T)) Snap { T x, y, z, r; };
 // alternate with the snapshots.  The generation of the table a step reads
 // sits in device memory (gen[step parity]); the step kernel writes the next
 // one, so graph replays need no host input.
-constexpr int LINE_WORDS = 32;               // uint32 words per bucket line
+//
+// Heads per line: the buckets are laid out in blocks of R = 1, 2 or 4
+// (Grid::super bits 25-26 = log2 R): a block's first 128-byte line holds
+// the heads of its R buckets (header and the first 32/R - 2 ids each), the
+// further ids of each follow in the block's other lines.  With R > 1 the
+// heads of neighbouring cells share lines (under the linear cell layout,
+// x-adjacent cells are adjacent buckets): fewer lines fetched per step.
+constexpr int LINE_WORDS = 32;               // uint32 words per bucket (head + further ids)
 constexpr int HEAD_WORDS = 2;                // the header's words
 constexpr int BUCKET_SLOTS = LINE_WORDS - HEAD_WORDS;
 constexpr uint32_t BOX_FLAG = 0x80000000u;   // set on ids of box bodies
 template <typename T> struct Table {
-    uint32_t *line;            // [H][LINE_WORDS]: header, then ids
+    uint32_t *line;            // [H / R][R x LINE_WORDS] bucket blocks: heads, then further ids
     Snap<T> *pos;              // [H][LINE_WORDS] slot snapshots (slot s at s); nullptr: not kept
     uint32_t *gen;             // this table's generation (device word)
 };
@@ -104,7 +111,8 @@ template <typename T> struct Grid {
     T inv_cs;                          // 1 / cell size
     uint32_t hmask;                    // H - 1 (H power of two)
     int32_t H;
-    int32_t super;                     // buckets grouped by super-cell, shape in nibbles (rb_grid.hpp bucket_of)
+    int32_t super;                     // buckets grouped by super-cell, shape in nibbles (rb_grid.hpp bucket_of);
+                                       // bits 25-26: log2 of the heads per line (Table)
 };
 
 template <typename T> struct StepParams {

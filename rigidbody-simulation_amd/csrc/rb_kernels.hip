@@ -167,7 +167,7 @@ __device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, 
 // (shuffles) places them — id and snapshot — in LDS, and the group
 // rank-sorts them by body id into s_id / s_pos.  Same contact set and order
 // as search_partners.
-template <typename T, int MAXP, int G, bool BOXES, typename Overlap>
+template <typename T, int MAXP, int G, bool BOXES, int RL, typename Overlap>
 __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool active, int32_t i, int32_t kind,
                                                V3<T> x, T rad, T bi, int32_t *s_id, Snap<T> *s_pos, int32_t *t_id,
                                                Snap<T> *t_pos, int slot, int k, int lane, uint32_t gen,
@@ -190,7 +190,8 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     // loaded unconditionally (b is a valid bucket for every lane) and the
     // count clamped only after overlap(): a use inside a branch would make
     // the wave wait for the loads before that work starts
-    const uint4 id4 = bucket_head(p.cur, b);
+    const int rl = RL >= 0 ? RL : grid_rl(p.grid.super);   // heads per line: cooperative worlds 1 (rb_capi.hip)
+    const uint4 id4 = bucket_head(p.cur, b, rl);
     Snap<T> p4[QS];
 #pragma unroll
     for (int u = 0; u < QS; ++u) p4[u] = p.cur.pos[base + u];
@@ -207,14 +208,14 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     uint32_t mask = 0;
 #pragma unroll
     for (int u = 0; u < QS; ++u)
-        if (u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u), p4[u], defer)) mask |= 1u << u;
+        if (u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, bucket_id(p.cur, b, id4, u, rl), p4[u], defer)) mask |= 1u << u;
     for (int s0 = QS; s0 < c; s0 += QB) {
         uint32_t tj[QB];
         Snap<T> sn[QB];
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
             if (s0 + u >= c) break;                   // stay inside this bucket's slots
-            tj[u] = bucket_id(p.cur, b, id4, s0 + u);
+            tj[u] = bucket_id(p.cur, b, id4, s0 + u, rl);
             sn[u] = p.cur.pos[base + s0 + u];
         }
 #pragma unroll
@@ -243,7 +244,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     for (int u = 0; u < QS; ++u) {
         if (!((mask >> u) & 1u)) continue;
         if (o < MAXP) {
-            t_id[slot * MAXP + o] = (int32_t)(bucket_id(p.cur, b, id4, u) & ~BOX_FLAG);
+            t_id[slot * MAXP + o] = (int32_t)(bucket_id(p.cur, b, id4, u, rl) & ~BOX_FLAG);
             t_pos[slot * MAXP + o] = p4[u];
         }
         ++o;
@@ -251,7 +252,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     for (uint32_t rest = mask & ~((1u << QS) - 1u); rest; rest &= rest - 1) {
         const int sl = __builtin_ctz(rest);
         if (o < MAXP) {                               // re-read: L1-hot from the batch above
-            t_id[slot * MAXP + o] = (int32_t)(bucket_id(p.cur, b, id4, sl) & ~BOX_FLAG);
+            t_id[slot * MAXP + o] = (int32_t)(bucket_id(p.cur, b, id4, sl, rl) & ~BOX_FLAG);
             t_pos[slot * MAXP + o] = p.cur.pos[base + sl];
         }
         ++o;
@@ -462,12 +463,14 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // next step's broadphase: the slot atomic goes first (a later load or
     // atomic would wait for every older store), its round trip overlaps the
     // snapshot store and the quaternion update
-    Claim cl{0u, 0, 0ull, 0u};
+    Claim cl{0u, 0, 0ull, 0u, 0};
     // the one-lane and wide forms (and the split form's update) run in
     // linear-layout worlds only; the cooperative form and the box kernel
     // read the layout
     constexpr int L = (PM == 2 || (PM == 0 && !BOXES)) ? LAYOUT_LINEAR : LAYOUT_ANY;
-    if (p.next.line) cl = claim_slot<L>(p.grid, p.next, p.err, sn, gen_next);
+    // heads per line: known in the cooperative and wide forms (rb_capi.hip)
+    constexpr int RL = PM == 1 ? 0 : PM == 2 ? 2 : -1;
+    if (p.next.line) cl = claim_slot<L, RL>(p.grid, p.next, p.err, sn, gen_next);
     wt_store(p.snap_next + i, sn);
     if (p.bounds) {                              // halo exchange: this body's new cell
         int32_t cx, cy, cz;
@@ -490,7 +493,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
         T *qs = p.quat_next + 4 * (int64_t)i;
         wt_store(qs + 0, qn.w); wt_store(qs + 1, qn.x); wt_store(qs + 2, qn.y); wt_store(qs + 3, qn.z);
     }
-    publish_slot(p.next, p.err, cl, sn, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
+    publish_slot<RL>(p.next, p.err, cl, sn, (uint32_t)i | (kind != 0 ? BOX_FLAG : 0u));
     STAMP(6);
 }
 
@@ -553,7 +556,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
         if (RB_ABLATE != 1) np_ = search_partners<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, tid, gen, defer);
     } else {
         if (RB_ABLATE != 1)
-            np_ = search_coop<T, MAXP, G, BOXES>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
+            np_ = search_coop<T, MAXP, G, BOXES, 0>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
                                           gen, defer, [&] {
                                               invI.get();
                                               if (!p.xfrc) {
@@ -735,7 +738,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void search_kernel(StepParams<T> p) {
     int32_t np_;
     bool defer = false;                          // split form: sphere worlds only
     if constexpr (G == 1) np_ = search_partners<T, MAXP, false>(p, i, kind, x, rad, self.r, s_id, tid, gen, defer);
-    else np_ = search_coop<T, MAXP, G, false>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
+    else np_ = search_coop<T, MAXP, G, false, -1>(p, active, i, kind, x, rad, self.r, s_id, s_pos, t_id, t_pos, slot, k, tid,
                                        gen, defer, [] {});
     if (!active) return;
     for (int s = k; s < np_; s += G) p.plist[CHK((int64_t)s * p.S + l, (int64_t)MAXP * p.S)] = s_id[s * NB + slot];

@@ -52,7 +52,7 @@ def run_one(sc):
 
 
 res = {}
-for rnd in range(2):
+for rnd in range(int(os.environ.get("ROUNDS", "2"))):
     for v in variants:
         _lib._lib = None
         _lib.load(paths[v])
