@@ -260,7 +260,12 @@ template <typename T> hipError_t launch_ball_step(const StepParams<T> &p, int ma
 template <typename T> hipError_t launch_ball_prime(const StepParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_kat_pair_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 
-constexpr int STEP_BLOCK = 64;
+// threads per step-kernel workgroup (the Makefile's WIDE_BLOCK sets it for
+// the wide form's unit alone)
+#ifndef RB_STEP_BLOCK
+#define RB_STEP_BLOCK 64
+#endif
+constexpr int STEP_BLOCK = RB_STEP_BLOCK;
 
 // lanes per body of the split form's search kernel (1, or 8 = the
 // cooperative search, which reads the bucket slot snapshots)
