@@ -381,6 +381,11 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
 #define RB_WIDE_LDSPOS 1
 #endif
 constexpr int WIDE_HPOS = 8;
+// diagnostic (0): the wide search skips buckets' ids past the head (wrong
+// for a bucket of 7+ bodies); measures the rare path's code footprint
+#ifndef RB_WIDE_MORE
+#define RB_WIDE_MORE 1
+#endif
 
 template <int MAXP, typename T>
 __device__ __forceinline__ void list_insert_pos(int32_t *s_id, uint8_t *s_didx, Snap<T> *s_hpos, int stride, int slot,
@@ -500,16 +505,27 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     batch(0);
     for (int base = QB; base < n; base += QB) batch(base);
     STAMP(9);
-    if (more) {
-        // buckets of 7+ bodies: the remaining ids from their lines, QB at a time
+    if (RB_WIDE_MORE && more) {
+        // buckets of 7+ bodies: the remaining ids from their lines, QB at a
+        // time.  Rare, so kept compact: the buckets and counts go to the
+        // lane's LDS column (s_cand is free now) and the loop over them is
+        // not unrolled (unrolled, this path was 132 KB of the kernel's 194 KB)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            for (int s0 = WIDE_HEAD_IDS; s0 < c[k]; s0 += QB) {
+            s_cand[k * NB + tid] = b[k];
+            s_cand[(8 + k) * NB + tid] = (uint32_t)c[k];
+        }
+#pragma unroll 1
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t bk = s_cand[k * NB + tid];
+            const int32_t ck = (int32_t)s_cand[(8 + k) * NB + tid];
+#pragma unroll 1
+            for (int s0 = WIDE_HEAD_IDS; s0 < ck; s0 += QB) {
                 uint32_t tj[QB];
                 Snap<T> sn[QB];
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
-                    tj[u] = s0 + u < c[k] ? *slot_word(p.cur, b[k], s0 + u, rl) : (uint32_t)i;
+                    tj[u] = s0 + u < ck ? *slot_word(p.cur, bk, s0 + u, rl) : (uint32_t)i;
 #pragma unroll
                 for (int u = 0; u < QB; ++u) {
                     sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
@@ -517,7 +533,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 }
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
-                    if (s0 + u < c[k] && hit(tj[u], sn[u])) {
+                    if (s0 + u < ck && hit(tj[u], sn[u])) {
                         if (RB_WIDE_LDSPOS)
                             list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u],
                                                   overflow);

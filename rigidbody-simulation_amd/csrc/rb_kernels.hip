@@ -379,16 +379,19 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     }
 
     // ---- K2: sphere partners in ascending id order ---------------------------
-    // (partner snapshots fetched 4 at a time; the solve itself is the
-    // reference's sequential Gauss-Seidel)
-    for (int s0 = 0; s0 < np_; s0 += 4) {
-        int32_t jj[4];
-        Snap<T> pe[4];
+    // (partner snapshots fetched PB at a time; the solve itself is the
+    // reference's sequential Gauss-Seidel).  The box kernel takes them one at
+    // a time: each unrolled copy of the loop body inlines the box
+    // narrowphase (4 copies made the kernel 169 KB)
+    constexpr int PB = BOXES ? 1 : 4;
+    for (int s0 = 0; s0 < np_; s0 += PB) {
+        int32_t jj[PB];
+        Snap<T> pe[PB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < PB; ++u)
             if (s0 + u < np_) jj[u] = pid[CHK((s0 + u) * stride, 32 * stride)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PB; ++u) {
             if (s0 + u >= np_) continue;
             if constexpr (PM == 1) {
                 pe[u] = ppos[(s0 + u) * stride];
@@ -400,7 +403,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PB; ++u) {
             if (s0 + u >= np_) break;
             const int32_t j = jj[u];
             const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};

@@ -374,6 +374,31 @@ def test_wide_form_on_contact_rich_scene_bit_exact(rb, oracle, monkeypatch):
     assert (kin == 16).sum() > 100
 
 
+def test_wide_form_buckets_past_the_head_bit_exact(rb, oracle, monkeypatch):
+    """The wide form's rare path: buckets of 7+ bodies, whose ids past the
+    32-byte head (6 ids) are read from the bucket's further lines.  A flat
+    grid at spacing 0.15 puts up to 9 landed spheres in one 0.4-m cell; 120
+    steps, then one recorded step, contacts and state bit-exact with the
+    oracle, and the scene is checked to hold such cells."""
+    from rbhip import scenes
+    monkeypatch.setenv("RBHIP_COOP_MAX_BODIES", "0")
+    sc = scenes.flat_spheres(33, 31, seed=5, spacing=0.15)
+    q0, v0, (cnt, par, kin, dis) = _oracle_run(oracle, sc, 121, record=True)
+    with rb.World(sc) as w:
+        w.step(120)
+        w.record_contacts(True)
+        w.step(1)
+        q, v = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert np.array_equal(gd, dis)
+    assert np.array_equal(q, q0) and np.array_equal(v, v0)
+    # cells (2 x 2 r = 0.4 m) holding 7+ bodies: the path is exercised
+    cells = np.floor(q0.reshape(-1, 7)[:, :3] / 0.4).astype(np.int64)
+    _, per_cell = np.unique(cells, axis=0, return_counts=True)
+    assert per_cell.max() >= 7
+
+
 @pytest.mark.parametrize("form,env", [
     ("coop", {}),
     ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
