@@ -84,6 +84,11 @@ struct rb_world {
     // 16k: 11.5 vs 14.4 us the other way)
     int64_t coop_max = 20480;
     int64_t wide_max = 65536;   // above coop_max, up to which the wide one-lane form is used
+    // owned bodies up to which the cooperative form runs with a helper wave
+    // per workgroup (inv(I_w), gravity and plane contacts off the body
+    // lanes' chain): 4k 8.1 -> 7.4 us, 8k 9.6 -> 8.6; 16k 11.0 -> 11.9 the
+    // other way (its waves then share SIMDs)
+    int64_t help_max = 12288;
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};
     double inv_cs = 1.0;
@@ -271,7 +276,8 @@ int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, doubl
         HIPCHK(r);
         return RB_OK;
     }
-    const int form = w->n_local <= w->coop_max ? FORM_COOP : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
+    const int form = w->n_local <= w->coop_max ? (w->n_local <= w->help_max ? FORM_COOP_HELP : FORM_COOP)
+                     : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
     if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, form, w->boxes, s);
     else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, form, w->boxes, s);
     HIPCHK(r);
@@ -692,6 +698,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxrec = 4 * w->n_planes + (any_box ? 4 : 1) * w->maxp;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
+    if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
     // snapshot line per bucket) 16 per body; the one-lane and wide forms
     // (linear cell groups, below) 32 per body, so the groups' period spans

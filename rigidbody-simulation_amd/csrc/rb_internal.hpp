@@ -243,7 +243,7 @@ template <typename T> struct HaloParams {
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one
 // lane per body at one wave per SIMD (mid-size scenes)
-enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2 };
+enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3 };
 // boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
 // the wide form's kernel alone (its own translation unit: scheduled for memory clauses)

@@ -337,7 +337,8 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                                             V3<T> sz, T bi, const BodyIn<T> &in, bool forced, LazyInvI<T> &invI,
                                             int32_t np_, const int32_t *pid, int64_t stride, const Snap<T> *ppos,
                                             int tid, int32_t *cell, uint32_t gen_next, T *poly = nullptr,
-                                            int ps = 0, const uint8_t *pdidx = nullptr) {
+                                            int ps = 0, const uint8_t *pdidx = nullptr, int32_t nrec_in = 0,
+                                            bool planes_done = false) {
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
@@ -348,9 +349,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     const T k = impulse_k(m);
 
     STAMP(3);
-    int32_t nrec = 0;
+    int32_t nrec = nrec_in;
     // ---- K2: plane contacts, plane order -------------------------------------
-    if (kind == 0) {
+    // (a sphere's already solved by the helper wave when planes_done)
+    if (kind == 0 && !planes_done) {
         for (int pl = 0; pl < p.n_planes; ++pl) {
             const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
             const V3<T> pp = {p.pp[pl][0], p.pp[pl][1], p.pp[pl][2]};
@@ -503,12 +505,13 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
 // One body (G lanes): contact search, then (lane 0) the update.  WIDE: the
 // one-lane form for one wave per SIMD (search_buckets_wide; state loads and
 // inv(I_w) under the head loads).
-template <typename T, int MAXP, int G, bool WIDE, bool BOXES, bool PRE = false>
+template <typename T, int MAXP, int G, bool WIDE, bool BOXES, bool PRE = false, bool HELP = false>
 __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> &ld, bool active, int64_t lb, int slot,
                                           int k, int tid,
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
                                           uint32_t *s_cand, int32_t *cell, uint32_t gen, T *s_poly,
-                                          uint8_t *s_didx = nullptr, Snap<T> *s_hpos = nullptr) {
+                                          uint8_t *s_didx = nullptr, Snap<T> *s_hpos = nullptr,
+                                          const T *s_help = nullptr) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = ld.lo + l;
@@ -557,6 +560,11 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
             });
     } else if constexpr (G == 1) {
         if (RB_ABLATE != 1) np_ = search_partners<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, tid, gen, defer);
+    } else if constexpr (HELP) {
+        // the helper wave evaluates inv(I_w) and gravity (help_body)
+        if (RB_ABLATE != 1)
+            np_ = search_coop<T, MAXP, G, BOXES, 0>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
+                                                    gen, defer, [] {});
     } else {
         if (RB_ABLATE != 1)
             np_ = search_coop<T, MAXP, G, BOXES, 0>(p, active, i, kind, x, sz.x, bi, s_id, s_pos, t_id, t_pos, slot, k, tid,
@@ -580,10 +588,29 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
         invI.I = in.I;
         invI.q = in.q;
     }
+    bool help_planes = false;
+    int32_t help_nrec = 0;
+    if constexpr (HELP) {
+        // the helper's results (its LDS writes precede the search's barriers)
+        const T *o = s_help + slot;
+        constexpr int NBH = STEP_BLOCK / G;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) invI.m.a[e] = o[e * NBH];
+        invI.have = true;
+        if (!p.xfrc) {
+            in.v = {o[9 * NBH], o[10 * NBH], o[11 * NBH]};
+            in.w = {o[12 * NBH], o[13 * NBH], o[14 * NBH]};
+            forced = true;
+        }
+        const T pr = o[15 * NBH];
+        help_planes = pr >= T(0);
+        help_nrec = help_planes ? (int32_t)pr : 0;
+    }
     constexpr int PM = G > 1 ? 1 : (WIDE && RB_WIDE_LDSPOS) ? 2 : 0;
     body_update<T, PM, BOXES>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB,
                               PM == 2 ? s_hpos + slot : s_pos + slot, tid, cell, gen + 1u,
-                              BOXES ? s_poly + slot : nullptr, NB, PM == 2 ? s_didx + slot : nullptr);
+                              BOXES ? s_poly + slot : nullptr, NB, PM == 2 ? s_didx + slot : nullptr, help_nrec,
+                              help_planes);
 }
 
 // Halo exchange: fold the wave's new cells (cell[0] == INT32_MAX: none) into
@@ -611,7 +638,58 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
     }
 }
 
-template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false>
+// Helper wave of the cooperative form (HELP): one lane per body of the
+// workgroup evaluates inv(I_w), gravity and a sphere's plane contacts (the
+// first in its contact order) — VALU chain the body lanes otherwise run
+// under or after their bucket loads — and leaves inv(I_w), v, w and the
+// recorded-contact count in LDS (column layout, 16 reals per body) before
+// the search's first barrier; it then takes part in the search's two
+// barriers.  The same arithmetic in the same order, so bit-identical.
+template <typename T, int NB>
+__device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> &ld, int h, T *s_help) {
+    const int64_t hb = (int64_t)blockIdx.x * NB + h;
+    if (h < NB && hb < ld.n_local) {
+        const int32_t l = (int32_t)hb, i = ld.lo + l;
+        BodyIn<T> in = load_body(ld.st, ld.cs, l, i);
+        LazyInvI<T> invI;
+        invI.I = in.I;
+        invI.q = in.q;
+        const M3<T> m = invI.get();
+        int32_t nrec = 0;
+        bool planes = false;
+        if (!p.xfrc) {
+            apply_force(p, l, in.m, invI, in.v, in.w);
+            // a sphere's plane contacts come first in its contact order
+            // (body_update), so they are solved here too
+            const int32_t kind = ld.cs.kind[i];
+            if (kind == 0) {
+                const Snap<T> self = ld.snap_cur[i];
+                const V3<T> x = {self.x, self.y, self.z};
+                const T rad = ld.cs.sx()[i];
+                const T k = impulse_k(in.m);
+                for (int pl = 0; pl < p.n_planes; ++pl) {
+                    const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
+                    const V3<T> pp = {p.pp[pl][0], p.pp[pl][1], p.pp[pl][2]};
+                    Contact<T> con;
+                    if (!plane_sphere(pn, pp, x, rad, con)) continue;
+                    record(p, l, nrec, -1 - pl, 0, con.dist);
+                    solve_contact(p, con, x, con.frame, in.m, k, invI, in.v, in.w);
+                }
+                planes = true;
+            }
+        }
+        T *o = s_help + h;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) o[e * NB] = m.a[e];
+        o[9 * NB] = in.v.x; o[10 * NB] = in.v.y; o[11 * NB] = in.v.z;
+        o[12 * NB] = in.w.x; o[13 * NB] = in.w.y; o[14 * NB] = in.w.z;
+        o[15 * NB] = T(planes ? nrec : -1);
+    }
+    __syncthreads();                             // search_coop's two barriers
+    __syncthreads();
+}
+
+template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false, bool HELP = false>
 __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> &ld) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
@@ -622,8 +700,16 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
+    __shared__ T s_help[HELP ? 16 * NB : 1];
     const int tid = threadIdx.x;
     if (RB_ABLATE == 3) return;
+    if constexpr (HELP) {
+        static_assert(G > 1 && !WIDE && !BOXES, "helper waves: the cooperative sphere form");
+        if (tid >= STEP_BLOCK) {                 // the workgroup's second wave
+            help_body<T, NB>(p, ld, tid - STEP_BLOCK, s_help);
+            return;
+        }
+    }
     STAMP(0);
 #if RB_STAMPS
     // placement: HW_ID (wave, SIMD, CU, SE fields) and XCC_ID of the block's first wave
@@ -644,8 +730,8 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     const bool active = lb < ld.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
     if (G > 1 || active)
-        body_step<T, MAXP, G, WIDE, BOXES, true>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand, cell,
-                                                 0u /* loaded in body_step */, s_poly, s_didx, s_hpos);
+        body_step<T, MAXP, G, WIDE, BOXES, true, HELP>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand,
+                                                       cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, s_help);
     if (p.bounds) fold_bounds(p.bounds, cell);
     if (blockIdx.x == 0 && tid == 0) {
         if (p.next.line) *p.next.gen = *p.cur.gen + 1u;
@@ -670,6 +756,16 @@ __attribute__((amdgpu_waves_per_eu(MAXP <= 16 ? RB_MIN_WAVES_COOP : 2)))   // 32
 void step_kernel_coop(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
                       const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
     step_body<T, MAXP, 8, false, false>(
+        p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
+}
+// the cooperative form with a helper wave per workgroup (help_body): small
+// scenes, whose body waves leave SIMDs idle
+template <typename T, int MAXP>
+__global__ __launch_bounds__(2 * STEP_BLOCK)
+__attribute__((amdgpu_waves_per_eu(MAXP <= 16 ? RB_MIN_WAVES_COOP : 2)))
+void step_kernel_coop_help(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
+                           const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
+    step_body<T, MAXP, 8, false, false, true>(
         p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
 }
 template <typename T, int MAXP>
@@ -866,7 +962,7 @@ __global__ __launch_bounds__(64) void kat_narrow_kernel(int64_t n, const double 
 
 // ---- launchers ----------------------------------------------------------
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s) {
-    const bool coop = form == FORM_COOP;
+    const bool coop = form == FORM_COOP || form == FORM_COOP_HELP;
     const int nb = coop ? STEP_BLOCK / 8 : STEP_BLOCK;
     int64_t blocks = (p.n_local + nb - 1) / nb;
     if (blocks < 1) blocks = 1;
@@ -881,6 +977,9 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
         if (maxp <= 16) hipLaunchKernelGGL((search_kernel<T, 16, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
+    } else if (coop && form == FORM_COOP_HELP && !boxes) {
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop_help<T, 16>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+        else hipLaunchKernelGGL((step_kernel_coop_help<T, 32>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     } else if (coop) {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
         else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);

@@ -401,6 +401,7 @@ def test_wide_form_buckets_past_the_head_bit_exact(rb, oracle, monkeypatch):
 
 @pytest.mark.parametrize("form,env", [
     ("coop", {}),
+    ("coop_help", {"RBHIP_HELP_MAX_BODIES": "100000"}),
     ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
     ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"}),
     ("split", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0", "RBHIP_SPLIT": "1"}),
