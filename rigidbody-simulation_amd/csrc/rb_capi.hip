@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <tuple>
@@ -845,34 +846,119 @@ int rb_set_stream(rb_world *w, void *s) {
     return RB_OK;
 }
 
-// The linear cell layout's period (rb_grid.hpp bucket_linear): split the
-// table's group bits over x, y, z by the scene's extent in groups, one bit
-// at a time to the axis the period covers least, so a scene folds onto
-// itself only when the table is too small for it (4M flat spheres, 8
-// buckets per body: 1.33 -> 0.87 ms per step; 32k on a 128 x 256 grid:
-// 18.8 -> 13.4 us).  Deterministic in the global positions, so every rank
-// of a sharded world picks the same split.
+// The linear cell layout's period (rb_grid.hpp bucket_linear): how the
+// table's group bits split over x, y, z.  A split folds the scene onto
+// itself where two groups a search reads (the occupied groups and their
+// neighbours) land on one run of buckets with at least one of them occupied:
+// those buckets then hold bodies of both, i.e. false candidates.  Every
+// split is scored by that count of colliding groups and the least is taken;
+// ties go to the split that leaves the fewest axes folded (a sheet folded
+// along one axis stays collision-free as it moves; folded along two, only
+// while the fold happens to miss it), then to the one whose period covers
+// the scene's extent most evenly.
+// Splitting by extent alone (one bit at a time to the axis the period covers
+// least) folded a sheet-like scene — C4's spheres on the incline, whose
+// bounding box is deep in z but whose groups are one layer thick — in x and
+// y to cover z: 14.8 -> 18.1 us per step; counting collisions keeps C4's
+// layout and still fits 4M flat spheres (1.33 -> 0.87 ms) and 32k on a
+// 128 x 256 grid (17.9 -> 13.2 us).  Deterministic in the global positions,
+// so every rank of a sharded world picks the same split.
 static void fit_period(rb_world *w, const double *qpos) {
     if (!((w->group >> 24) & 1)) return;                 // hashed layouts have no period
+    if (const char *ev = getenv("RBHIP_FIT_PERIOD"))
+        if (atoi(ev) == 0) return;                       // diagnostic: keep the creation-time split
     const int gb[3] = {w->group & 15, (w->group >> 4) & 15, (w->group >> 8) & 15};
     const int lg = ((w->group >> 12) & 15) + ((w->group >> 16) & 15) + ((w->group >> 20) & 15);
+    constexpr int64_t OFF = 1 << 20;                     // group coordinates kept in [-2^20, 2^20)
+    auto pack = [](int64_t gx, int64_t gy, int64_t gz) {
+        return ((gx + OFF) << 42) | ((gy + OFF) << 21) | (gz + OFF);
+    };
+    auto unpack = [](int64_t k, int d) { return ((k >> (42 - 21 * d)) & ((1 << 21) - 1)) - OFF; };
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-    for (int64_t b = 0; b < w->N; ++b)
+    std::vector<int64_t> occ;
+    occ.reserve((size_t)w->N);
+    for (int64_t b = 0; b < w->N; ++b) {
+        int64_t g[3];
+        bool ok = true;
         for (int d = 0; d < 3; ++d) {
             const double c = qpos[7 * b + d] * w->inv_cs;
-            if (c == c && c > -1e9 && c < 1e9) { lo[d] = c < lo[d] ? c : lo[d]; hi[d] = c > hi[d] ? c : hi[d]; }
+            if (!(c == c && c > -1e9 && c < 1e9)) { ok = false; break; }
+            lo[d] = c < lo[d] ? c : lo[d];
+            hi[d] = c > hi[d] ? c : hi[d];
+            g[d] = (int64_t)floor(c) >> gb[d];
+            if (g[d] <= -OFF + 1 || g[d] >= OFF - 1) ok = false;
         }
+        if (ok) occ.push_back(pack(g[0], g[1], g[2]));
+    }
+    std::sort(occ.begin(), occ.end());
+    occ.erase(std::unique(occ.begin(), occ.end()), occ.end());
+    // the groups a search reads: the occupied ones and their neighbours
+    // (flag bit 0: occupied)
+    // (above 8,192 occupied groups the occupied ones alone: the split search
+    // stays well under a second at 4M bodies)
+    std::vector<int64_t> q;
+    q.reserve(occ.size() * 27);
+    if (occ.size() > 8192) q = occ;
+    else for (int64_t k : occ)
+        for (int dz = -1; dz <= 1; ++dz)
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx)
+                    q.push_back(pack(unpack(k, 0) + dx, unpack(k, 1) + dy, unpack(k, 2) + dz));
+    std::sort(q.begin(), q.end());
+    q.erase(std::unique(q.begin(), q.end()), q.end());
+    std::vector<int64_t> qg[3];
+    std::vector<uint8_t> qocc(q.size());
+    for (int d = 0; d < 3; ++d) qg[d].resize(q.size());
+    for (size_t t = 0; t < q.size(); ++t) {
+        for (int d = 0; d < 3; ++d) qg[d][t] = unpack(q[t], d);
+        qocc[t] = std::binary_search(occ.begin(), occ.end(), q[t]) ? 1 : 0;
+    }
     double need[3];
     for (int d = 0; d < 3; ++d)
         need[d] = hi[d] >= lo[d] ? (floor(hi[d]) - floor(lo[d]) + 2) / double(1 << gb[d]) : 1.0;
-    int l[3] = {0, 0, 0};
-    for (int k = 0; k < lg; ++k) {
-        int best = 0;
-        for (int d = 1; d < 3; ++d)
-            if (need[d] / double(1 << l[d]) > need[best] / double(1 << l[best]) + 1e-12) best = d;
-        ++l[best];
-    }
-    const int32_t g = (w->group & ~(0xfff << 12)) | (l[0] << 12) | (l[1] << 16) | (l[2] << 20);
+    std::vector<uint64_t> f(q.size());
+    int best[3] = {(w->group >> 12) & 15, (w->group >> 16) & 15, (w->group >> 20) & 15};
+    int64_t best_c = -1;
+    int best_nf = 0;
+    double best_fold = 0.0;
+    for (int lx = 0; lx <= lg && lx <= 15; ++lx)
+        for (int ly = 0; lx + ly <= lg && ly <= 15; ++ly) {
+            const int lz = lg - lx - ly;
+            if (lz > 15) continue;
+            const int l[3] = {lx, ly, lz};
+            for (size_t t = 0; t < q.size(); ++t) {
+                uint64_t idx = 0;
+                int sh = 0;
+                for (int d = 0; d < 3; ++d) {
+                    idx |= ((uint64_t)qg[d][t] & ((1ull << l[d]) - 1)) << sh;
+                    sh += l[d];
+                }
+                f[t] = (idx << 1) | qocc[t];
+            }
+            std::sort(f.begin(), f.end());
+            int64_t coll = 0;
+            for (size_t a = 0; a < f.size();) {
+                size_t e = a;
+                bool any_occ = false;
+                while (e < f.size() && (f[e] >> 1) == (f[a] >> 1)) any_occ |= (f[e++] & 1);
+                if (any_occ) coll += (int64_t)(e - a) - 1;
+                a = e;
+            }
+            double fold = 0.0;
+            int nf = 0;                                  // axes the period does not cover
+            for (int d = 0; d < 3; ++d) {
+                fold = std::max(fold, need[d] / double(1 << l[d]));
+                nf += need[d] > double(1 << l[d]);
+            }
+            if (best_c < 0 || coll < best_c || (coll == best_c && nf < best_nf) ||
+                (coll == best_c && nf == best_nf && fold < best_fold - 1e-12)) {
+                best_c = coll;
+                best_nf = nf;
+                best_fold = fold;
+                best[0] = lx; best[1] = ly; best[2] = lz;
+            }
+        }
+    const int32_t g = (w->group & ~(0xfff << 12)) | (best[0] << 12) | (best[1] << 16) | (best[2] << 20);
     if (g != w->group) {
         w->group = g;
         drop_graphs(w);                                  // the grid is a captured kernel argument
