@@ -155,35 +155,67 @@ def cpu_baseline(cfg: str, steps: int):
     return base, ref
 
 
+def _pairs(cnt, par):
+    """(body, partner) pairs of a CSR contact list."""
+    import numpy as np
+    body = np.repeat(np.arange(cnt.size), cnt)
+    return set(zip(body.tolist(), par.tolist()))
+
+
 def accuracy(cfg: str, dtype: str, device: int, steps: int, ref) -> dict:
-    """GPU state after `steps` steps from t = 0 vs the fp64 oracle run
-    (BASELINE metric "CPU-ref max|Δpos|"; the state written at
-    multi_sphere_bounce.py:85-88) and the last step's contact lists."""
+    """GPU state against the fp64 oracle (BASELINE metric "CPU-ref max|Δpos|";
+    the state written at multi_sphere_bounce.py:85-88) from t = 0: at
+    `steps` (the cpu_baseline run, `ref`) and, for fp32 (the
+    fp32 vs fp64 sweep), also at steps 1, 10 and 100 — max / median relative
+    position error and the contact-flip count (body-partner contacts present
+    in one run's last-step list and not the other's)."""
     import numpy as np
     import rbhip
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
     sc, _ = make_scene(cfg, 1, "strong")
-    q_ref, v_ref, (cnt, par, kin, dis) = ref
+    osc = O.OracleScene(sc)
+    checkpoints = sorted({1, 10, 100, steps} if dtype == "f32" else {steps})
+    checkpoints = [c for c in checkpoints if c <= steps]
+    rows = []
+    qo, vo = sc.qpos0.copy(), sc.qvel0.copy()
     with rbhip.World(sc, device=device, dtype=dtype) as w:
-        if steps > 1:
-            w.step(steps - 1)
         w.record_contacts(True)
-        w.step(1)
-        q, v = w.get_state()
-        gc, gp, gk, _ = w.contacts()
-    dx = np.linalg.norm(q[:, :3] - q_ref[:, :3], axis=1)
-    dv = np.linalg.norm(v - v_ref, axis=1)
-    rel_x = dx / np.maximum(np.linalg.norm(q_ref[:, :3], axis=1), 1e-12)
-    rel_v = dv / np.maximum(np.linalg.norm(v_ref, axis=1), 1e-12)
-    return {"vs": "oracle fp64 (cpu_baseline run), same initial conditions",
-            "steps": steps, "dtype": dtype,
-            "max_abs_dpos": float(np.abs(q[:, :3] - q_ref[:, :3]).max()),
-            "max_rel_dpos": float(rel_x.max()), "max_rel_dvel": float(rel_v.max()),
-            "median_rel_dpos": float(np.median(rel_x)),
-            "contacts_equal": bool(np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)),
-            "contacts_last_step": int(cnt.sum()),
-            "bit_identical": bool(np.array_equal(q.view(np.uint64), q_ref.view(np.uint64)) and
-                                  np.array_equal(v.view(np.uint64), v_ref.view(np.uint64))),
-            "definition": "rel = |d| / |ref| per body (position 3-vector; velocity 6-vector incl. spin)"}
+        done = 0
+        for c in checkpoints:
+            if c == steps:
+                q_ref, v_ref, (cnt, par, kin, dis) = ref
+            else:
+                qo, vo, (cnt, par, kin, dis) = O.step(osc, qo, vo, c - done, record=True)
+                q_ref, v_ref = qo, vo
+            w.step(c - done)
+            done = c
+            q, v = w.get_state()
+            gc, gp, gk, _ = w.contacts()
+            dx = np.linalg.norm(q[:, :3] - q_ref[:, :3], axis=1)
+            dv = np.linalg.norm(v - v_ref, axis=1)
+            rel_x = dx / np.maximum(np.linalg.norm(q_ref[:, :3], axis=1), 1e-12)
+            rel_v = dv / np.maximum(np.linalg.norm(v_ref, axis=1), 1e-12)
+            flips = len(_pairs(gc, gp) ^ _pairs(cnt, par))
+            rows.append({"step": c, "max_abs_dpos": float(np.abs(q[:, :3] - q_ref[:, :3]).max()),
+                         "max_rel_dpos": float(rel_x.max()), "median_rel_dpos": float(np.median(rel_x)),
+                         "max_rel_dvel": float(rel_v.max()), "contact_flips": flips,
+                         "contacts_ref": int(cnt.sum()),
+                         "contacts_equal": bool(np.array_equal(gc, cnt) and np.array_equal(gp, par) and
+                                                np.array_equal(gk, kin)),
+                         "bit_identical": bool(np.array_equal(q.view(np.uint64), q_ref.view(np.uint64)) and
+                                               np.array_equal(v.view(np.uint64), v_ref.view(np.uint64)))})
+    last = rows[-1]
+    out = {"vs": "oracle fp64 (cpu_baseline run), same initial conditions, from t = 0",
+           "steps": steps, "dtype": dtype,
+           **{k: last[k] for k in ("max_abs_dpos", "max_rel_dpos", "max_rel_dvel", "median_rel_dpos",
+                                   "contacts_equal", "bit_identical", "contact_flips")},
+           "contacts_last_step": last["contacts_ref"],
+           "definition": "rel = |d| / |ref| per body (position 3-vector; velocity 6-vector incl. spin); "
+                         "contact_flips = |pairs(gpu) xor pairs(oracle)| of the checkpoint step"}
+    if len(rows) > 1:
+        out["sweep"] = rows
+    return out
 
 
 class SingleWorldCheck:
@@ -232,14 +264,13 @@ class SingleWorldCheck:
         return bool(int(t.item()))
 
 
-def step_kernel_name(n_owned: int) -> str:
-    """The step kernel form the library picks for n_owned bodies
-    (rb_capi.hip launch_one: coop <= 20,480 < wide <= 65,536 < one)."""
-    if n_owned <= int(os.environ.get("RBHIP_COOP_MAX_BODIES", "20480")):
-        return "rb::step_kernel_coop"
-    if n_owned <= int(os.environ.get("RBHIP_WIDE_MAX_BODIES", "65536")):
-        return "rb::step_kernel_wide"
-    return "rb::step_kernel_one"
+def step_kernel_name(stats: dict, tiled: bool) -> str:
+    """The kernel that stepped the timed region, as the library reports it
+    (rb_world_stats): the tile-block kernel, or the per-step form."""
+    from rbhip import _lib
+    if tiled:
+        return "rb::tile_block_kernel"
+    return _lib.FORM_NAMES.get(stats.get("form"), "?")
 
 
 def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str):
@@ -339,6 +370,7 @@ def main():
     sw.step(args.steps)              # capture the K-step graph outside the timed region
     sw.sync()
     barrier_sync()
+    st0 = w.stats()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()                      # the library enqueues on torch's current stream
@@ -348,6 +380,8 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
+    st1 = w.stats()
+    tiled = st1.get("tile_steps", 0) > st0.get("tile_steps", 0)
     timed = [done + args.steps + 1, done + 2 * args.steps]
     if P > 1:
         t = torch.tensor([elapsed], device=dev_red, dtype=torch.float64)
@@ -360,7 +394,13 @@ def main():
     # region is exactly K back-to-back step-kernel launches (graph replay),
     # so HIP events around it / K.  Several ranks: a step also runs the
     # exchange, so time each step-kernel launch with its own event pair.
-    if P == 1:
+    if P == 1 and tiled:
+        # K-step tile blocks: one launch steps up to kmax reference steps;
+        # the timed region is the run's launches (gather, blocks, write-back)
+        avg_ms, launches = region_ms / args.steps, st1["tile_blocks"] - st0["tile_blocks"]
+        timing = ("HIP events around the timed region / K steps (tile blocks: achieved = algorithmic bytes of "
+                  "the K committed steps / region time)")
+    elif P == 1:
         avg_ms, launches, timing = region_ms / args.steps, args.steps, "HIP events around the timed region / K"
     else:
         w.kernel_timing(True)
@@ -398,11 +438,18 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": traffic_lower,
                      "traffic_source": traffic_src,
-                     "kernel": step_kernel_name(w.n_owned),
+                     "kernel": step_kernel_name(st1, tiled),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
+    if tiled:
+        line["roofline"]["algorithmic_bytes_per_launch"] = None
+        line["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
+        line["tile"] = {k: st1[k] - st0[k] for k in ("tile_blocks", "tile_redo_taint", "tile_redo_bound",
+                                                      "tile_restart", "tile_fallback", "tile_steps")}
+        line["tile"].update({k: st1[k] for k in ("tiles", "tile_threads", "tile_kmax", "tile_cap")})
+        line["tile"]["tile_size_m"] = st1["tile_size_um"] * 1e-6
     if rank == 0 and P == 1 and not args.no_cpu_baseline:
         w.close()
         base, ref = cpu_baseline(args.config, args.cpu_steps)

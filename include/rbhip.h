@@ -264,6 +264,37 @@ int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in,
  * average device duration (ms) of the step kernel over the launches timed
  * since the last reset (HIP events on the world's stream; enable first). */
 int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
+
+/* K-step tile blocks (no reference counterpart: the reference steps one
+ * frame per call, multi_sphere_bounce.py:42).  Sphere worlds on one rank
+ * step blocks of up to kmax reference steps per kernel launch: each tile of
+ * the scene plus a ghost band of width `band` is stepped in on-chip memory,
+ * and a block is committed only when it is provably identical to single
+ * steps (else redone shorter) -- results are bit-identical either way.
+ * mode -1 = auto (scenes of >= 16,384 bodies; env RBHIP_TILE overrides),
+ * 0 = off, 1 = on; kmax / band (m) / owned (target bodies per tile): 0
+ * keeps the current value.  Refits the tile grid to the current positions. */
+int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned);
+
+/* Counters for tests and measurement; fills out[0 .. min(n, RB_STATS_COUNT))
+ * and returns how many: */
+#define RB_STAT_GRAPHS        0   /* captured step graphs alive               */
+#define RB_STAT_TILE_RUNS     1   /* rb_step calls that ran tile blocks        */
+#define RB_STAT_TILE_BLOCKS   2   /* tile block launches that did work         */
+#define RB_STAT_TILE_REDO_T   3   /* blocks redone: an owned body was tainted  */
+#define RB_STAT_TILE_REDO_B   4   /* blocks redone: a body left its bound      */
+#define RB_STAT_TILE_RESTART  5   /* blocks rebuilt at horizon 1               */
+#define RB_STAT_TILE_FALLBACK 6   /* runs finished on the per-step kernels     */
+#define RB_STAT_TILE_STEPS    7   /* steps committed by tile blocks            */
+#define RB_STAT_FORM          8   /* per-step kernel form (0 one-lane, 1 cooperative, 2 wide, 3 cooperative + helper) */
+#define RB_STAT_TILES         9   /* tiles of the grid                         */
+#define RB_STAT_TILE_THREADS 10   /* threads (stepped bodies) per tile         */
+#define RB_STAT_TILE_KMAX    11
+#define RB_STAT_TILE_CAP     12   /* bodies per tile bin                       */
+#define RB_STAT_TILE_SIZE_UM 13   /* tile edge in micrometres                  */
+#define RB_STAT_TILE_ON      14   /* a long rb_step would use tile blocks now  */
+#define RB_STATS_COUNT       15
+int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 
 #ifdef __cplusplus

@@ -647,7 +647,8 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
 // barriers.  The same arithmetic in the same order, so bit-identical.
 template <typename T, int NB>
 __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> &ld, int h, T *s_help) {
-    const int64_t hb = (int64_t)blockIdx.x * NB + h;
+    // the same block -> bodies mapping as the body lanes (step_body)
+    const int64_t hb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + h;
     if (h < NB && hb < ld.n_local) {
         const int32_t l = (int32_t)hb, i = ld.lo + l;
         BodyIn<T> in = load_body(ld.st, ld.cs, l, i);

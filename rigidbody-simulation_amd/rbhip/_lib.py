@@ -72,7 +72,16 @@ SIGNATURES = {
     "rb_set_contact_law": (C.c_int, [_P, _I32, _D]),
     "rb_query": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     "rb_kernel_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(_I64)]),
+    "rb_tile_config": (C.c_int, [_P, _I32, _I32, _D, _I64]),
+    "rb_world_stats": (C.c_int, [_P, C.POINTER(_I64), _I32]),
 }
+
+# rb_world_stats indices (include/rbhip.h RB_STAT_*)
+STAT_NAMES = ["graphs", "tile_runs", "tile_blocks", "tile_redo_taint", "tile_redo_bound", "tile_restart",
+              "tile_fallback", "tile_steps", "form", "tiles", "tile_threads", "tile_kmax", "tile_cap",
+              "tile_size_um", "tile_on"]
+FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
+              3: "rb::step_kernel_coop_help"}
 
 _lib = None
 

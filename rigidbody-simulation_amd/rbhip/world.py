@@ -202,6 +202,21 @@ class World:
         t = tot.value
         return cnt, par[:t], kin[:t], dis[:t]
 
+    def tile_config(self, mode: int = -1, kmax: int = 0, band: float = 0.0, owned: int = 0):
+        """K-step tile blocks (rb_tile_config): mode -1 auto, 0 off, 1 on;
+        kmax / band (m) / owned bodies per tile, 0 = keep."""
+        _lib.check(self._L.rb_tile_config(self._h, int(mode), int(kmax), float(band), int(owned)), "rb_tile_config")
+
+    def stats(self) -> dict:
+        """Counters of the world (rb_world_stats): tile blocks, redos, the
+        per-step kernel form, ..."""
+        n = len(_lib.STAT_NAMES)
+        buf = (C.c_int64 * n)()
+        rc = self._L.rb_world_stats(self._h, buf, n)
+        if rc < 0:
+            _lib.check(rc, "rb_world_stats")
+        return {k: int(buf[i]) for i, k in enumerate(_lib.STAT_NAMES[:rc])}
+
     def kernel_timing(self, enable: bool):
         """Toggle per-launch HIP-event timing of the step kernel; returns the
         (average ms, launches) collected since it was last enabled."""
