@@ -64,6 +64,12 @@ extern "C" {
 #define RB_CK_PLANE_SPHERE   0
 #define RB_CK_PLANE_BOX0     1   /* 1 + corner index (0..7, corner bits i&1,i&2,i&4) */
 #define RB_CK_SPHERE_SPHERE 16
+/* Box-involved kinds are this project's restatement of MuJoCo's sphere-box /
+ * box-box primitives (not available offline): parity against MuJoCo is
+ * UNPINNED (the reference's only box, models/cube.xml:35, never meets
+ * another box or a sphere).  Known divergence: a face contact keeps at most
+ * the 4 deepest clipped points, where mjc_BoxBox may return more and select
+ * differently. */
 #define RB_CK_SPHERE_BOX    17   /* sphere = geom1 (MuJoCo dispatches by geom type) */
 #define RB_CK_BOX_BOX0      32   /* 32 + k: k-th face-clip point of a box pair (k < 4) */
 #define RB_CK_BOX_EDGE      40   /* edge-edge point of a box pair */
@@ -271,7 +277,8 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
  * the scene plus a ghost band of width `band` is stepped in on-chip memory,
  * and a block is committed only when it is provably identical to single
  * steps (else redone shorter) -- results are bit-identical either way.
- * mode -1 = auto (scenes of >= 16,384 bodies; env RBHIP_TILE overrides),
+ * mode -1 = auto (currently: off -- measured no faster than the per-step
+ * kernels on the BASELINE scenes; env RBHIP_TILE overrides),
  * 0 = off, 1 = on; kmax / band (m) / owned (target bodies per tile): 0
  * keeps the current value.  Refits the tile grid to the current positions. */
 int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned);

@@ -102,6 +102,8 @@ struct rb_world {
     double prm_dt = 0, prm_e = 0, prm_mu = 0;   // the ground phase held in the snapshots (two-ball law)
     int64_t H = 4096;
     int32_t group = 0;             // Grid::super: bucket grouping shape (x | y << 4 | z << 8 bits)
+    bool fit_valid = false;        // fit_period: the group box (and layout) the last fit was made for
+    int64_t fit_key[7] = {};
     int64_t bytes_per_body_step = 0;
     // device memory
     void *snap[2] = {};        // [Npad] Snap<T>: (x, y, z, bound radius), ping-pong
@@ -148,17 +150,17 @@ struct rb_world {
     std::map<std::tuple<int64_t, int, double, double, double, double, int>, GraphEntry> graphs;
     uint64_t graph_tick = 0;
     // K-step tile blocks (rb_tile.hip): sphere worlds, one rank
+    // Auto mode is off until a scene size where the blocks beat the per-step
+    // kernels is measured (C3 about parity, 8k and 1M bodies slower)
     int tile_mode = -1;            // -1 auto (RBHIP_TILE), 0 off, 1 on
     int tile_kmax = 8;             // longest block
     double tile_band = 0;          // ghost band W (0: 10 x rmax)
-    int64_t tile_owned = 256;      // target owned bodies per tile
-    int64_t tile_min_bodies = 16384;   // auto mode: fewer bodies step with the per-step kernels
-    int tile_nt = 768;             // threads (= stepped bodies) per tile workgroup
+    int64_t tile_owned = 0;        // target owned bodies per tile (0: 160 in fp64, 256 in fp32)
+    int64_t tile_min_bodies = INT64_MAX;   // auto mode: fewer bodies step with the per-step kernels
+    int tile_nt = 512;             // threads (= stepped bodies) per tile workgroup (fp32: 768)
     int32_t tile_ntx = 0, tile_nty = 0, tile_cap = 0;
     double tile_ox = 0, tile_oy = 0, tile_size = 0;
-    void *tile_rec = nullptr;      // [2][ntile][TILE_NF][cap]
-    float *tile_sig = nullptr;     // [2][ntile][cap]
-    int32_t *tile_id = nullptr;    // [2][ntile][cap]
+    void *tile_rec = nullptr;      // [2][ntile][cap] TileRec<T>
     int32_t *tile_count = nullptr; // [2][ntile]
     TileCtl *tile_ctl = nullptr;
     TileCtl *tile_ctl_host = nullptr;   // pinned: [0] the run's initial control word, [1] read back
@@ -503,9 +505,7 @@ bool tile_eligible(const rb_world *w, int64_t nsteps) {
 
 template <typename T> TileParams<T> make_tile(rb_world *w, double dt, double e, double mu, double thr) {
     TileParams<T> p{};
-    p.rec = dp<T>(w->tile_rec, 0);
-    p.sig = w->tile_sig;
-    p.id = w->tile_id;
+    p.rec = reinterpret_cast<TileRec<T> *>(w->tile_rec);
     p.count = w->tile_count;
     p.ctl = w->tile_ctl;
     p.ntx = w->tile_ntx;
@@ -793,7 +793,7 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *tbufs[] = {w->tile_rec, w->tile_sig, w->tile_id, w->tile_count, w->tile_ctl};
+    void *tbufs[] = {w->tile_rec, w->tile_count, w->tile_ctl};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_ctl_host) (void)hipHostFree(w->tile_ctl_host);
@@ -1071,6 +1071,23 @@ static void fit_period(rb_world *w, const double *qpos) {
         }
         if (ok) occ.push_back(pack(g[0], g[1], g[2]));
     }
+    // the split depends on the occupied groups; a call whose groups span
+    // the same box as the last fit's (every frame of a per-frame caller:
+    // multi_sphere_bounce.py:42 runs once per frame) keeps that fit instead
+    // of re-sorting every split (RBHIP_FIT_PERIOD=2 always refits)
+    {
+        int64_t gb_lo[3] = {INT64_MAX, INT64_MAX, INT64_MAX}, gb_hi[3] = {INT64_MIN, INT64_MIN, INT64_MIN};
+        for (int64_t k : occ)
+            for (int d = 0; d < 3; ++d) {
+                gb_lo[d] = std::min(gb_lo[d], unpack(k, d));
+                gb_hi[d] = std::max(gb_hi[d], unpack(k, d));
+            }
+        const int64_t key[7] = {gb_lo[0], gb_lo[1], gb_lo[2], gb_hi[0], gb_hi[1], gb_hi[2], (int64_t)w->group};
+        const char *ev = getenv("RBHIP_FIT_PERIOD");
+        if (w->fit_valid && memcmp(key, w->fit_key, sizeof key) == 0 && !(ev && atoi(ev) == 2)) return;
+        memcpy(w->fit_key, key, sizeof key);
+        w->fit_valid = true;
+    }
     std::sort(occ.begin(), occ.end());
     occ.erase(std::unique(occ.begin(), occ.end()), occ.end());
     // the groups a search reads: the occupied ones and their neighbours
@@ -1144,6 +1161,7 @@ static void fit_period(rb_world *w, const double *qpos) {
         w->group = g;
         drop_graphs(w);                                  // the grid is a captured kernel argument
     }
+    w->fit_key[6] = (int64_t)w->group;
 }
 
 // Tile grid of the K-step blocks (rb_tile.hip): square xy tiles sized for
@@ -1153,6 +1171,9 @@ static void fit_period(rb_world *w, const double *qpos) {
 // the edge tiles (unbounded outward).
 static int fit_tiles(rb_world *w, const double *qpos) {
     if (w->P != 1 || !w->all_spheres || w->tile_mode == 0) return RB_OK;
+    // auto mode allocates the bins only for scenes it would tile
+    if (w->tile_mode < 0 && w->N < w->tile_min_bodies) { w->tile_ntx = 0; return RB_OK; }
+    w->tile_nt = w->dtype == RB_F64 ? 512 : 768;
     double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
     int64_t nf = 0;
     for (int64_t b = 0; b < w->N; ++b) {
@@ -1165,7 +1186,8 @@ static int fit_tiles(rb_world *w, const double *qpos) {
     if (!nf) { w->tile_ntx = 0; return RB_OK; }
     const double band = w->tile_band > 0 ? w->tile_band : 10.0 * w->rmax;
     const double ex = std::max(hi[0] - lo[0], 1e-9), ey = std::max(hi[1] - lo[1], 1e-9);
-    double T = sqrt(ex * ey * (double)w->tile_owned / (double)w->N);
+    const int64_t owned = w->tile_owned > 0 ? w->tile_owned : (w->dtype == RB_F64 ? 160 : 256);
+    double T = sqrt(ex * ey * (double)owned / (double)w->N);
     T = std::max(T, std::max(2.5 * band, 8.0 * w->rmax));
     int64_t ntx = 0, nty = 0;
     for (;; T *= 1.1) {
@@ -1187,13 +1209,12 @@ static int fit_tiles(rb_world *w, const double *qpos) {
     w->tile_cap_grow = false;
     const int64_t ntile = ntx * nty;
     if (ntile * cap != (int64_t)w->tile_ntx * w->tile_nty * w->tile_cap || !w->tile_rec) {
-        void *old[] = {w->tile_rec, w->tile_sig, w->tile_id, w->tile_count};
+        void *old[] = {w->tile_rec, w->tile_count};
         for (void *b : old)
             if (b) HIPCHK(hipFree(b));
-        w->tile_rec = nullptr; w->tile_sig = nullptr; w->tile_id = nullptr; w->tile_count = nullptr;
-        HIPCHK(hipMalloc(&w->tile_rec, (size_t)w->esz * 2 * ntile * TILE_NF * cap));
-        HIPCHK(hipMalloc((void **)&w->tile_sig, sizeof(float) * 2 * ntile * cap));
-        HIPCHK(hipMalloc((void **)&w->tile_id, sizeof(int32_t) * 2 * ntile * cap));
+        w->tile_rec = nullptr; w->tile_count = nullptr;
+        const size_t rec = w->dtype == RB_F64 ? sizeof(TileRec<double>) : sizeof(TileRec<float>);
+        HIPCHK(hipMalloc(&w->tile_rec, rec * 2 * ntile * cap));
         HIPCHK(hipMalloc((void **)&w->tile_count, sizeof(int32_t) * 2 * ntile));
     }
     if (!w->tile_ctl) HIPCHK(hipMalloc((void **)&w->tile_ctl, sizeof(TileCtl)));

@@ -252,7 +252,6 @@ template <typename T> struct HaloParams {
 // bound; otherwise the block is redone from the same start, shorter.
 // Bodies are stored per tile ("bins"), in the tile that owned them at the
 // last block start; bins ping-pong with the block parity.
-constexpr int TILE_NF = 13;            // record reals: x y z qw qx qy qz vx vy vz wx wy wz
 constexpr int TILE_MAXL = 16;          // neighbour-list entries per body
 constexpr int TILE_NCOL = 1024;        // LDS columns of the list build
 constexpr int32_t ERR_TILE = 1 << 20;  // tile capacity / band exhausted (host falls back; never user-visible)
@@ -273,13 +272,20 @@ struct TileCtl {
     uint32_t acc_sig;                  // max over owned bodies of the new speed bound
     uint32_t acc_done;                 // workgroups finished
     int32_t acc_disp;                  // a displacement bound was left (statistics)
-    int32_t pad;
+    int32_t streak;                    // clean blocks in a row at the current horizon
+};
+
+// One body in a tile bin (array of structures: a lane moves its body with
+// 16-byte accesses; the bin pass reads x, y with one)
+template <typename T> struct alignas(16) TileRec {
+    T x, y, z, qw, qx, qy, qz, vx, vy, vz, wx, wy, wz;   // state
+    T m, ix, iy, iz, r;                                // constants (mass, principal inertia, radius)
+    int32_t id;                                        // global id
+    float sig;                                         // top speed over the owner's last block
 };
 
 template <typename T> struct TileParams {
-    T *rec;                            // [2][ntile][TILE_NF][cap] body records, per tile
-    float *sig;                        // [2][ntile][cap] speed bound (max |v| over the owner's last block)
-    int32_t *id;                       // [2][ntile][cap] global ids
+    TileRec<T> *rec;                   // [2][ntile][cap] body records, per tile
     int32_t *count;                    // [2][ntile]
     TileCtl *ctl;
     int32_t ntile, ntx, nty, cap;

@@ -50,6 +50,8 @@ def main():
     out = {"config": a.config, "us_per_step": el / a.steps * 1e6, "wg_blocks": buf[8],
            "mean_k_run": buf[9] / n, "mean_stepped": buf[10] / n, "mean_outer": buf[11] / n,
            "cycles_per_wg": {names[k]: buf[k] / n for k in range(1, 6)},
+           "active_lanes_per_wg_step": buf[14] / max(buf[9], 1), "active_waves_per_wg_step": buf[15] / max(buf[9], 1),
+           "lists_split": {"columns": buf[12] / n, "scan": buf[13] / n, "sort": (buf[3] - 0) / n},
            "tile": {k: s1[k] - s0[k] for k in ("tile_blocks", "tile_redo_taint", "tile_redo_bound", "tile_restart",
                                                 "tile_fallback", "tile_steps")}}
     print(json.dumps(out), flush=True)

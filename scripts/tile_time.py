@@ -2,8 +2,9 @@
 
     python scripts/tile_time.py [--config c3] [--warmup 450] [--steps 400] [--k 8] [--band 0] [--owned 256]
 
-For each mode: a fresh World, `warmup` steps, then `steps` timed steps (host
-wall clock around one synchronous rb_step), with the world's counters
+For each mode: a fresh World, `warmup` steps, `steps` untimed steps (the
+per-step path captures its graph there), then `steps` timed steps (host wall
+clock around one synchronous rb_step), with the world's counters
 (blocks, redos, fallbacks).  Checks that both modes end bit-identical.
 """
 from __future__ import annotations
@@ -34,12 +35,17 @@ def main():
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--modes", default="0,1")
     a = ap.parse_args()
-    sc = scenes.make(a.config)
+    if a.config.startswith("flat:"):                 # flat:NXxNY (C3's layout, e.g. one 8-GPU slab: flat:256x32)
+        nx, ny = (int(v) for v in a.config[5:].split("x"))
+        sc = scenes.flat_spheres(nx, ny)
+    else:
+        sc = scenes.make(a.config)
     res = {}
     for mode in [int(m) for m in a.modes.split(",")]:
         with rbhip.World(sc, dtype=a.dtype) as w:
             w.tile_config(mode, a.k, a.band, a.owned)
             w.step(a.warmup)
+            w.step(a.steps)                   # capture the per-step graph outside the timed region
             s0 = w.stats()
             t0 = time.perf_counter()
             w.step(a.steps)
@@ -50,7 +56,7 @@ def main():
                                          "tile_fallback", "tile_steps")}
         res[mode] = (q, v)
         print(json.dumps({"config": a.config, "dtype": a.dtype, "tile_mode": mode, "bodies": sc.n,
-                          "timed_steps": [a.warmup + 1, a.warmup + a.steps], "us_per_step": el / a.steps * 1e6,
+                          "timed_steps": [a.warmup + a.steps + 1, a.warmup + 2 * a.steps], "us_per_step": el / a.steps * 1e6,
                           "body_steps_per_s": sc.n * a.steps / el, "tiles": s1["tiles"], "tile_kmax": s1["tile_kmax"],
                           "tile_size_m": s1["tile_size_um"] * 1e-6, **d}), flush=True)
     if len(res) == 2:

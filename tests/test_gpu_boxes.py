@@ -57,13 +57,16 @@ def test_kat_narrow_f32_matches_f32_restatement(rb, oracle):
     assert np.array_equal(rb.kat_narrow(inp, dtype="f32"), oracle.kat_narrow(inp, dtype="f32"))
 
 
-@pytest.mark.parametrize("form,env", [("coop", {}), ("one", {"RBHIP_COOP_MAX_BODIES": "0"})])
+@pytest.mark.parametrize("form,env", [("coop", {}), ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+                                      ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"})])
 def test_box_pile_bit_exact(rb, oracle, monkeypatch, form, env):
     """Tilted cube columns with sphere caps (rbhip.scenes.box_pile) landing,
     stacking, leaning and toppling: every step of two recorded windows
     (contacts and state) and the state every 100 steps bit-exact with the
     oracle over 600 steps, with face-clip, edge-edge and sphere-box contacts
-    all present — through the cooperative and the one-lane box forms."""
+    all present — through the cooperative, wide and one-lane sphere forms
+    (each followed by the box kernel; "one" is what every box world above
+    65,536 bodies runs)."""
     from rbhip import scenes
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -122,7 +125,8 @@ def _approaching_boxes():
                         qpos, qvel, dt=0.01, restitution=0.5, friction=0.4, threshold=0.0)
 
 
-@pytest.mark.parametrize("form,env", [("coop", {}), ("one", {"RBHIP_COOP_MAX_BODIES": "0"})])
+@pytest.mark.parametrize("form,env", [("coop", {}), ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+                                      ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"})])
 def test_boxes_entering_range_bit_exact(rb, oracle, monkeypatch, form, env):
     """Boxes stepped by the sphere kernel (no box partner in range) must
     still publish their orientation for the step a box pair comes into

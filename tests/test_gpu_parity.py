@@ -277,19 +277,30 @@ def test_graph_equals_single_launches_and_reruns(rb):
         assert np.array_equal(q, res[0][0]) and np.array_equal(v, res[0][1])
 
 
-@pytest.mark.parametrize("P", [2, 3, 4])
-def test_shard_invariance_in_process(rb, P):
+@pytest.mark.parametrize("P,scene,steps", [(2, "flat800", 120), (3, "flat800", 120), (4, "flat800", 120),
+                                           (8, "c4", 240)])
+def test_shard_invariance_in_process(rb, P, scene, steps):
     """P body-range shards on one device, positions exchanged by device copies
-    between their replicated buffers: bit-identical to one world."""
+    between their replicated buffers: bit-identical (uint64 words) to one
+    world, and the last step's contact lists equal.  (8, "c4") is BASELINE
+    configs[3] as the 8-GPU run shards it: 65,536 spheres on the incline,
+    8,192 per rank (the body loop of multi_sphere_bounce.py:46-90 split by
+    body-id range)."""
     import torch
     from rbhip import scenes
     from rbhip.shard import wrap_gpos
-    sc = scenes.flat_spheres(32, 25, seed=7)          # N = 800 (not a multiple of 3)
+    sc = scenes.flat_spheres(32, 25, seed=7) if scene == "flat800" else scenes.make(scene)   # 800: not a multiple of 3
     with rb.World(sc) as ref:
-        ref.step(120)
+        ref.step(steps - 1)
+        ref.record_contacts(True)
+        ref.step(1)
         rq, rv = ref.get_state()
+        rc, rp, rk, rd = ref.contacts()
     worlds = [rb.World(sc, rank=r, world_size=P) for r in range(P)]
-    for _ in range(120):
+    for s in range(steps):
+        if s == steps - 1:
+            for w in worlds:
+                w.record_contacts(True)
         for w in worlds:
             w.shard_step()
         for w in worlds:
@@ -305,10 +316,16 @@ def test_shard_invariance_in_process(rb, P):
             w.shard_exchange_done()
     q = np.zeros((sc.n, 7))
     v = np.zeros((sc.n, 6))
+    cnt, par, kin, dis = [], [], [], []
     for w in worlds:
         w.get_state(q, v)
+        c, pa, k, d = w.contacts()
+        cnt.append(c); par.append(pa); kin.append(k); dis.append(d)
         w.close()
-    assert np.array_equal(q, rq) and np.array_equal(v, rv)
+    assert np.array_equal(q.view(np.uint64), rq.view(np.uint64)) and np.array_equal(v.view(np.uint64), rv.view(np.uint64))
+    assert np.array_equal(np.concatenate(cnt), rc) and np.array_equal(np.concatenate(par), rp)
+    assert np.array_equal(np.concatenate(kin), rk)
+    assert np.array_equal(np.concatenate(dis).view(np.uint64), rd.view(np.uint64))
 
 
 # ---------------------------------------------------------------- loud failures

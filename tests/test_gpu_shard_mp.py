@@ -20,6 +20,12 @@ def _free_port():
     return p
 
 
+def _scene(P, patch):
+    from rbhip import scenes
+    # patch == "c4": BASELINE configs[3] split by body-id range (strong scaling)
+    return scenes.make("c4") if patch == "c4" else scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2)
+
+
 def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
@@ -27,9 +33,8 @@ def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=P)
-    from rbhip import scenes
     from rbhip.shard import ShardedWorld
-    sc = scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2)
+    sc = _scene(P, patch)
     sw = ShardedWorld(sc, device=0, transport=transport, halo=halo)
     assert sw.transport == transport and sw.halo == halo
     sw.step(steps)
@@ -43,7 +48,8 @@ def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
 
 @pytest.mark.parametrize("P,transport,halo,patch", [(2, "host", False, 16), (2, "p2p", False, 16),
                                                     (3, "p2p", False, 16), (2, "p2p", True, 16),
-                                                    (3, "p2p", True, 16), (2, "p2p", True, 96)])
+                                                    (3, "p2p", True, 16), (2, "p2p", True, 96),
+                                                    (2, "p2p", True, "c4"), (2, "p2p", False, "c4")])
 def test_two_process_shards_match_single_world(tmp_path, P, transport, halo, patch):
     """Several processes on one GPU; "p2p" maps the other processes' buffers
     through IPC and synchronises on device flags, as across GPUs; halo=True
@@ -53,7 +59,7 @@ def test_two_process_shards_match_single_world(tmp_path, P, transport, halo, pat
     import rbhip
     from rbhip import scenes
     steps = 80
-    sc = scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2)
+    sc = _scene(P, patch)
     with rbhip.World(sc) as w:
         w.step(steps)
         q1, v1 = w.get_state()

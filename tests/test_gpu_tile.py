@@ -116,17 +116,19 @@ def test_tile_bodies_leaving_the_grid(rb, oracle):
     assert_same(q, v, q1, v1, f"fliers ({st})")
 
 
-def test_tile_auto_mode_and_off(rb):
-    """Auto mode takes large sphere worlds only; mode 0 keeps the per-step
-    kernels (the counters say which ran)."""
+def test_tile_modes_and_counters(rb):
+    """Mode 1 takes sphere worlds; mode 0 keeps the per-step kernels; auto
+    mode is currently off; box worlds never tile.  The
+    counters say which ran."""
     with rb.World(scenes.make("c3")) as w:
+        assert w.stats()["tile_on"] == 0          # auto: off
+        w.tile_config(1)
         assert w.stats()["tile_on"] == 1
         w.step(16)
         assert w.stats()["tile_steps"] == 16
         w.tile_config(0)
         w.step(16)
         assert w.stats()["tile_steps"] == 16 and w.stats()["tile_on"] == 0
-    with rb.World(scenes.make("c2")) as w:
-        assert w.stats()["tile_on"] == 0          # 4,096 bodies: per-step kernels
     with rb.World(scenes.make("c5")) as w:
+        w.tile_config(1)
         assert w.stats()["tile_on"] == 0          # boxes: per-step kernels
