@@ -169,6 +169,7 @@ struct rb_world {
     double tile_prm[4] = {};       // dt, e, mu, thr of the pending run
     int64_t tile_stats[8] = {};    // runs, blocks, redo (taint), redo (bound), restarts, fallbacks, steps, capacity refits
     bool tile_cap_grow = false;    // a run stopped on a tile's capacity: refit with more room
+    double tile_room = 1.1;        // growth allowance of the fullest tile's band (raised by each capacity stop)
     // kernel timing
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
@@ -587,6 +588,7 @@ int tile_start(rb_world *w, int64_t n, double dt, double e, double mu, double th
 
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false,
                   bool allow_tile = true);
+int tile_refit(rb_world *w);
 
 // Wait for the run in flight; continue it if redos used up the spare blocks;
 // on a capacity stop, finish on the per-step kernels.
@@ -612,9 +614,18 @@ int tile_finish(rb_world *w) {
     // the device stopped early (a tile's capacity, the band): the rest on the
     // per-step kernels, from the committed state the write-back left
     w->tile_stats[5] += 1;
-    if (c.err & ERR_TILE) w->tile_cap_grow = true;
     const double *q = w->tile_prm;
-    return enqueue_steps(w, w->tile_target - c.done, q[0], q[1], q[2], q[3], false, false);
+    int rc = enqueue_steps(w, w->tile_target - c.done, q[0], q[1], q[2], q[3], false, false);
+    if (rc) return rc;
+    if (c.err & ERR_TILE) {
+        // a tile outgrew its lanes or bins: refit to the positions now, with
+        // more room, before the next run
+        w->tile_cap_grow = true;
+        w->tile_room *= 1.25;
+        w->tile_stats[7] += 1;
+        return tile_refit(w);
+    }
+    return RB_OK;
 }
 
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
@@ -1189,20 +1200,32 @@ static int fit_tiles(rb_world *w, const double *qpos) {
     const int64_t owned = w->tile_owned > 0 ? w->tile_owned : (w->dtype == RB_F64 ? 160 : 256);
     double T = sqrt(ex * ey * (double)owned / (double)w->N);
     T = std::max(T, std::max(2.5 * band, 8.0 * w->rmax));
+    // a tile's band must fit the workgroup's lanes: the fullest tile's
+    // density over (T + 2W)^2, with room to grow, within 90 % of them
+    const double floorT = std::max(2.5 * band, 8.0 * w->rmax);
+    T = std::max(T, floorT);
     int64_t ntx = 0, nty = 0;
-    for (;; T *= 1.1) {
-        ntx = std::max<int64_t>(1, (int64_t)ceil(ex / T));
-        nty = std::max<int64_t>(1, (int64_t)ceil(ey / T));
-        if (ntx * nty <= 65535) break;
-    }
-    std::vector<int32_t> hist((size_t)(ntx * nty), 0);
     int32_t most = 0;
-    for (int64_t b = 0; b < w->N; ++b) {
-        const double x = qpos[7 * b], y = qpos[7 * b + 1];
-        int64_t tx = (int64_t)((x - lo[0]) / T), ty = (int64_t)((y - lo[1]) / T);
-        tx = tx < 0 ? 0 : tx >= ntx ? ntx - 1 : tx;
-        ty = ty < 0 ? 0 : ty >= nty ? nty - 1 : ty;
-        most = std::max(most, ++hist[(size_t)(ty * ntx + tx)]);
+    std::vector<int32_t> hist;
+    for (int attempt = 0;; ++attempt) {
+        for (;; T *= 1.1) {
+            ntx = std::max<int64_t>(1, (int64_t)ceil(ex / T));
+            nty = std::max<int64_t>(1, (int64_t)ceil(ey / T));
+            if (ntx * nty <= 65535) break;
+        }
+        hist.assign((size_t)(ntx * nty), 0);
+        most = 0;
+        for (int64_t b = 0; b < w->N; ++b) {
+            const double x = qpos[7 * b], y = qpos[7 * b + 1];
+            int64_t tx = (int64_t)((x - lo[0]) / T), ty = (int64_t)((y - lo[1]) / T);
+            tx = tx < 0 ? 0 : tx >= ntx ? ntx - 1 : tx;
+            ty = ty < 0 ? 0 : ty >= nty ? nty - 1 : ty;
+            most = std::max(most, ++hist[(size_t)(ty * ntx + tx)]);
+        }
+        const double loaded = (double)most / (T * T) * (T + 2 * band) * (T + 2 * band) * w->tile_room;
+        if (loaded <= 0.9 * w->tile_nt) break;
+        if (T <= floorT * 1.0001 || attempt > 40) { w->tile_ntx = 0; return RB_OK; }   // too dense to tile
+        T = std::max(floorT, T * 0.9);
     }
     int64_t cap = std::max<int64_t>(512, (2 * (int64_t)most + 63) / 64 * 64);
     if (w->tile_cap_grow) cap = std::max<int64_t>(cap, 2 * (int64_t)w->tile_cap);
@@ -1602,18 +1625,11 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
     return RB_OK;
 }
 
-int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned) {
-    if (!w) return fail(RB_EINVAL, "null world");
-    if (mode < -1 || mode > 1 || kmax < 0 || kmax > 64 || !(band >= 0) || owned < 0)
-        return fail(RB_EINVAL, "bad tile configuration");
-    HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
-    w->tile_mode = mode;
-    if (kmax) w->tile_kmax = kmax;
-    if (band > 0) w->tile_band = band;
-    if (owned) w->tile_owned = std::max<int64_t>(16, owned);
-    if (mode == 0 || w->P != 1 || !w->all_spheres) return RB_OK;
-    // refit the grid to the current positions (the snapshot of this step)
+}  // extern "C"
+
+namespace {
+// refit the tile grid to the positions of the current step (the snapshot)
+int tile_refit(rb_world *w) {
     std::vector<double> q((size_t)7 * w->N, 0.0);
     const size_t n = (size_t)4 * w->Npad;
     HIPCHK(hipStreamSynchronize(w->stream));
@@ -1627,6 +1643,23 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
         for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = s[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = s[(size_t)(4 * b + 1)]; }
     }
     return fit_tiles(w, q.data());
+}
+}  // namespace
+
+extern "C" {
+
+int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (mode < -1 || mode > 1 || kmax < 0 || kmax > 64 || !(band >= 0) || owned < 0)
+        return fail(RB_EINVAL, "bad tile configuration");
+    HIPCHK(hipSetDevice(w->device));
+    if (int rc = tile_finish(w)) return rc;
+    w->tile_mode = mode;
+    if (kmax) w->tile_kmax = kmax;
+    if (band > 0) w->tile_band = band;
+    if (owned) w->tile_owned = std::max<int64_t>(16, owned);
+    if (mode == 0 || w->P != 1 || !w->all_spheres) return RB_OK;
+    return tile_refit(w);
 }
 
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {

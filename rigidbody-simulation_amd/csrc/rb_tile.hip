@@ -341,17 +341,17 @@ __global__ __launch_bounds__(NT) void tile_block_kernel(TileParams<T> p) {
                 if (o < LC - NT) s_ref[NT + o] = cref[u];
                 else s_misc[2] = ERR_TILE;
             }
-            if (bl) {
-#pragma unroll
-                for (int c = 0; c < NQ; ++c) {
-                    const uint64_t bc = __ballot(isl && q == c);
-                    if (lane == c && bc) atomicAdd(&s_q[c], __popcll(bc));
-                }
-            }
         }
     }
     __syncthreads();
     const int nl = s_misc[0] < NT ? s_misc[0] : NT, no = s_misc[1] < LC - NT ? s_misc[1] : LC - NT;
+    // a tile over capacity (band or ring) steps nothing: the run stops and
+    // the host resumes on the per-step kernels (no entry may be left unset)
+    const bool over = s_misc[2] != 0;
+    if (!over) {
+    // the stored band entries in distance-class order (counted, scanned, placed)
+    if (tid < nl) atomicAdd(&s_q[s_key[tid]], 1);
+    __syncthreads();
     if (tid == 0) {
         int a = 0;
         for (int k = 0; k < NQ; ++k) { const int c = s_q[k]; s_q[k] = a; a += c; }
@@ -365,6 +365,9 @@ __global__ __launch_bounds__(NT) void tile_block_kernel(TileParams<T> p) {
     V3<T> x{}, v{}, w{};
     Q4<T> q{};
     bool own = false;
+    const uint32_t nref = (uint32_t)p.ntile * (uint32_t)p.cap;
+    if (tid < nl && s_ref[tid] >= nref) { s_ref[tid] = 0; atomicOr(&ctl->acc_err, ERR_TILE); }   // (never: defensive)
+    if (tid < no && s_ref[NT + tid] >= nref) { s_ref[NT + tid] = 0; atomicOr(&ctl->acc_err, ERR_TILE); }
     if (tid < nl) {
         const uint32_t ref = s_ref[tid];
         const TileRec<T> r = load_rec(p.rec + bin_at(p, ph, (int)(ref / (uint32_t)p.cap), (int)(ref % (uint32_t)p.cap)));
@@ -426,9 +429,6 @@ __global__ __launch_bounds__(NT) void tile_block_kernel(TileParams<T> p) {
         }
     }
     __syncthreads();
-    if (s_misc[2]) {                           // capacity: the run falls back
-        if (tid == 0) { atomicOr(&ctl->acc_err, s_misc[2]); s_misc[3] = 0; }
-    }
     TSTAMP(2);
     int my_valid = k_run;
     int disp_bad = 0;
@@ -783,6 +783,10 @@ __global__ __launch_bounds__(NT) void tile_block_kernel(TileParams<T> p) {
     }
 
     TSTAMP(5);
+    } else if (tid == 0) {                     // capacity: the run falls back
+        atomicOr(&ctl->acc_err, s_misc[2]);
+        s_misc[3] = 0;
+    }
 #if RB_TILE_STAMPS
     if (tid == 0) { atomicAdd(&rb_tile_stamp_sum[8], 1ull); atomicAdd(&rb_tile_stamp_sum[9], (unsigned long long)k_run);
                     atomicAdd(&rb_tile_stamp_sum[10], (unsigned long long)nl); atomicAdd(&rb_tile_stamp_sum[11], (unsigned long long)no); }
