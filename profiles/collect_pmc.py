@@ -38,6 +38,7 @@ def mean_for(vals, needle):
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     dtype = sys.argv[2] if len(sys.argv) > 2 else "f64"
+    P = int(sys.argv[3]) if len(sys.argv) > 3 else 1      # > 1: one rank's step kernel of a P-way strong split
     # calibration: known-byte kernel with the state access pattern
     exe = "/tmp/calib_fetch"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-o", exe,
@@ -48,15 +49,22 @@ def main():
     cw = mean_for(run_pmc("WRITE_SIZE", [exe, str(n)], "calib"), "soa_rw")
     read_factor = known / (cf * 1024.0)
     write_factor = known / (cw * 1024.0)
-    bench = [sys.executable, "bench.py", "--config", cfg, "--dtype", dtype, "--no-cpu-baseline",
-             "--steps", "200", "--warmup", "20"]
-    f = mean_for(run_pmc("FETCH_SIZE", bench, cfg), "step_kernel")
-    w = mean_for(run_pmc("WRITE_SIZE", bench, cfg), "step_kernel")
+    if P == 1:
+        bench = [sys.executable, "bench.py", "--config", cfg, "--dtype", dtype, "--no-cpu-baseline",
+                 "--steps", "200", "--warmup", "20"]
+    else:
+        # P shards stepped in one process (scripts/shard_step_run.py): each
+        # rank's step kernel over its own slice, tables as in a P-GPU run
+        bench = [sys.executable, "scripts/shard_step_run.py", "--config", cfg, "--dtype", dtype, "--P", str(P)]
+    tag = cfg if P == 1 else f"{cfg}_p{P}"
+    f = mean_for(run_pmc("FETCH_SIZE", bench, tag), "step_kernel")
+    w = mean_for(run_pmc("WRITE_SIZE", bench, tag), "step_kernel")
     guide = f * 1024.0 * 2.0 + w * 1024.0
     calibrated = f * 1024.0 * read_factor + w * 1024.0 * write_factor
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
-    data[f"{cfg}_{dtype}"] = {
+    key = f"{cfg}_{dtype}" if P == 1 else f"{cfg}_{dtype}_p{P}"
+    data[key] = {
         "fetch_size_kb_per_launch": f, "write_size_kb_per_launch": w,
         "hbm_bytes_per_launch": guide,
         "hbm_bytes_per_launch_lower": f * 1024.0 + w * 1024.0,
@@ -71,7 +79,7 @@ def main():
                 "hbm_bytes_per_launch_lower and hbm_bytes_per_launch",
     }
     json.dump(data, open(path, "w"), indent=1)
-    print(json.dumps(data[f"{cfg}_{dtype}"], indent=1))
+    print(json.dumps(data[key], indent=1))
 
 
 if __name__ == "__main__":

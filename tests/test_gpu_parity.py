@@ -217,18 +217,23 @@ def test_f32_bit_exact_vs_f32_restatement(rb, oracle):
     assert np.array_equal(q, q0) and np.array_equal(v, v0)
 
 
-def test_f32_vs_f64_tolerance_sweep(rb, oracle):
+@pytest.mark.parametrize("horizon,max_flip_frac,med_rel,max_d", [(1, 1e-3, 1e-6, 1e-3), (10, 1e-3, 1e-5, 1e-2)])
+def test_f32_vs_f64_tolerance_sweep(rb, oracle, horizon, max_flip_frac, med_rel, max_d):
     """C3 fp32-vs-fp64 sweep (SURVEY §8d, §7 hard part 5): from the same
-    evolved fp64 state, one step in each precision — contact flips (pairs
-    present in one list only) and the one-step state error; the long-horizon
-    divergence is reported, not asserted (contacts decided differently send
-    chaotic bodies on other trajectories)."""
+    evolved fp64 state, `horizon` steps in each precision — contact flips
+    (pairs present in one list only, last step) and the state error.  Bounds
+    are asserted at 1 and 10 steps (measured on MI355X: 0 flips, max rel
+    dpos 1.0e-7 / 6.2e-7); the 100- and 200-step divergence is reported by
+    bench.py's fp32 line (profiles/r03/bench_c3_f32.json), not asserted:
+    contacts decided differently send chaotic bodies on other trajectories."""
     from rbhip import scenes
     sc = scenes.make("c3")
     q, v = oracle.step(oracle.OracleScene(sc), sc.qpos0, sc.qvel0, 30)
     res = {}
     for dt in ("f64", "f32"):
         with rb.World(sc.with_(qpos0=q, qvel0=v), dtype=dt) as w:
+            if horizon > 1:
+                w.step(horizon - 1)
             w.record_contacts(True)
             w.step(1)
             qq, vv = w.get_state()
@@ -239,10 +244,10 @@ def test_f32_vs_f64_tolerance_sweep(rb, oracle):
     ncon = len(res["f64"][2])
     d = np.abs(res["f32"][0][:, :3] - res["f64"][0][:, :3])
     rel = d / (1.0 + np.abs(res["f64"][0][:, :3]))
-    print(f"\nC3 fp32 vs fp64, one step from step 30: {ncon} contacts, {flips} flips, "
+    print(f"\nC3 fp32 vs fp64, {horizon} step(s) from step 30: {ncon} contacts, {flips} flips, "
           f"median rel dpos {np.median(rel):.2e}, max |dpos| {d.max():.2e}")
-    assert ncon > 1000 and flips <= max(2, ncon // 1000)
-    assert np.median(rel) < 1e-6 and d.max() < 1e-3
+    assert ncon > 1000 and flips <= max(2, int(ncon * max_flip_frac))
+    assert np.median(rel) < med_rel and d.max() < max_d
 
 
 def test_xfrc_applied_matches_oracle(rb, oracle):
