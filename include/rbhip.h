@@ -39,7 +39,7 @@ extern "C" {
 #define RB_ENOMEM      (-12)  /* device or host allocation failed               */
 #define RB_ENODEV      (-19)  /* no HIP device / HIP runtime failure            */
 #define RB_EOVERFLOW   (-75)  /* contact or broadphase-bucket capacity exceeded */
-#define RB_EUNSUPPORTED (-95) /* unsupported combination (e.g. box pairs across shards) */
+#define RB_EUNSUPPORTED (-95) /* unsupported combination (e.g. the two-ball law in a sharded world) */
 #define RB_EDOM        (-33)  /* non-finite or out-of-range body position       */
 
 /* ---- enums ------------------------------------------------------------- */
@@ -161,6 +161,15 @@ int rb_shard_exchange_done(rb_world *w);
  * is the contiguous [rank][S][4] (shard_elems = 4*S elements). */
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems,
                    int32_t *elem_bytes);
+/* Worlds with box bodies: the orientation buffer the same exchange fills
+ * alongside (layout [P][S][4], (w, x, y, z) per body in global id order, rows
+ * of box bodies meaningful) — all-gather it like the position buffer.  A
+ * sphere-only world returns *dev_ptr = NULL and *shard_elems = 0 (nothing
+ * to exchange: a sphere's contacts never read its orientation).  No reference
+ * counterpart (the reference is single-process; its box body is
+ * models/cube.xml:35). */
+int rb_gquat_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems,
+                    int32_t *elem_bytes);
 
 /* In-library exchange: the library owns an RCCL communicator over the
  * world's ranks (RCCL is loaded at first use; the single-GPU path never
@@ -225,9 +234,9 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol);
  * default: recording costs HBM traffic).  Canonical per-body order: plane
  * contacts (plane order; box corners in bit order), then partners by
  * ascending body id (a box-involved partner: its contacts in generation
- * order, RB_CK_SPHERE_BOX / RB_CK_BOX_BOX0 + k / RB_CK_BOX_EDGE).  Box-
- * involved pairs are solved in unsharded worlds; a sharded world reports
- * one within contact range as RB_EUNSUPPORTED.  Output is CSR over the owned bodies: counts[n_owned];
+ * order, RB_CK_SPHERE_BOX / RB_CK_BOX_BOX0 + k / RB_CK_BOX_EDGE), in
+ * sharded worlds as well (their exchange carries the boxes' orientations:
+ * rb_gquat_buffer).  Output is CSR over the owned bodies: counts[n_owned];
  * partner (body id, or -1-plane_index), kind (RB_CK_*), dist.  cap is the
  * capacity of the flat arrays; total receives the number of records. */
 int rb_record_contacts(rb_world *w, int enable);
@@ -300,7 +309,12 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 #define RB_STAT_TILE_CAP     12   /* bodies per tile bin                       */
 #define RB_STAT_TILE_SIZE_UM 13   /* tile edge in micrometres                  */
 #define RB_STAT_TILE_ON      14   /* a long rb_step would use tile blocks now  */
-#define RB_STATS_COUNT       15
+#define RB_STAT_BOX_OPT      15   /* box worlds: chunks replayed without the box kernel */
+#define RB_STAT_BOX_ROLLBACK 16   /* of which rolled back and replayed with it (a body was deferred) */
+#define RB_STAT_REFITS       17   /* broadphase layout refits of a drifting scene (chunk rolled back, replayed) */
+#define RB_STAT_TABLE_GROWS  18   /* of which with the bucket table doubled */
+#define RB_STAT_BUCKETS      19   /* buckets per table now */
+#define RB_STATS_COUNT       20
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

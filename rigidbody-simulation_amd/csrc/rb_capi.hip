@@ -65,8 +65,7 @@ int err_to_code(int32_t bits) {
     if (bits & ERR_EXCHANGE) return fail(RB_ENODEV, "device: peer-to-peer exchange timed out (a peer rank did not reach the step)");
     if (bits & ERR_DOMAIN) return fail(RB_EDOM, "device: non-finite or out-of-range body position");
     if (bits & ERR_UNSUPPORTED)
-        return fail(RB_EUNSUPPORTED, "device: box-involved pair within contact range in a sharded world "
-                                     "(box orientations are not exchanged between shards)");
+        return fail(RB_EUNSUPPORTED, "device: box-involved pair within contact range with no box kernel to take it");
     if (bits & ERR_PARTNER_OVERFLOW) return fail(RB_EOVERFLOW, "device: a body has more sphere partners than max_partners");
     if (bits & ERR_BUCKET_OVERFLOW) return fail(RB_EOVERFLOW, "device: more than 30 bodies hashed to one broadphase bucket");
     return RB_OK;
@@ -95,12 +94,13 @@ struct rb_world {
     double inv_cs = 1.0;
     double rmax = 0.0;             // largest bounding radius
     bool all_spheres = true;
-    bool boxes = false;            // box-capable step kernels (box bodies, unsharded)
+    bool boxes = false;            // box-capable step kernels (any box body; sharded worlds exchange orientations)
     // contact law (rb_set_contact_law)
     int32_t law = RB_LAW_MUJOCO;
     double tol = 0.01;
     double prm_dt = 0, prm_e = 0, prm_mu = 0;   // the ground phase held in the snapshots (two-ball law)
     int64_t H = 4096;
+    int64_t hmax = 4096;           // the table's growth limit (RBHIP_HASH_MAX_BYTES)
     int32_t group = 0;             // Grid::super: bucket grouping shape (x | y << 4 | z << 8 bits)
     bool fit_valid = false;        // fit_period: the group box (and layout) the last fit was made for
     int64_t fit_key[7] = {};
@@ -110,6 +110,20 @@ struct rb_world {
     void *qsnap[2] = {};       // boxes: [Npad][4] step-start orientations, ping-pong with snap
     int32_t *defer_q = nullptr;    // boxes: [S] bodies the step kernel defers to the box kernel
     int32_t *defer_cnt = nullptr;  // boxes: [2] queue lengths by step parity
+    // box worlds, one rank: chunks of steps replay optimistically WITHOUT the
+    // box kernel (an idle one still costs a kernel boundary per step); the
+    // step kernels then only count deferrals, and a chunk that deferred any
+    // body is rolled back to its start and replayed with the box kernel
+    bool box_opt = true;           // RBHIP_BOX_OPTIMISTIC=0: always launch the box kernel
+    bool box_kernel_on = true;     // launch_one: the box kernel follows the step kernel
+    int32_t box_backoff = 0;       // chunks to run with the box kernel after a rollback (doubles)
+    int32_t box_skip = 0;          // of which left
+    void *opt_save = nullptr;      // chunk-start copy: state rows, snapshot, orientations, error word
+    int32_t *defer_host = nullptr; // pinned [2]
+    int64_t box_stats[2] = {};     // optimistic chunks, rollbacks
+    bool sync_call = false;        // inside rb_step (synchronous): long chunks are guarded
+    int64_t refits = 0;            // layout refits after a bucket overflow (rolled back, replayed)
+    int64_t table_grows = 0;       // of which with the table doubled
     void *state = nullptr;     // 13 x S  (qw qx qy qz vx vy vz wx wy wz px py pz)
     void *vel[2] = {};         // two-ball law: [Npad] Vel<T>, ping-pong with the snapshots
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
@@ -133,6 +147,7 @@ struct rb_world {
     int32_t *push_cnt = nullptr;   // halo: [P] bodies pushed to each peer this step
     int64_t *epoch = nullptr;      // steps taken since connect (advanced by the step kernel)
     void **peer_snap_dev = nullptr;       // [2][P] device array: each rank's snapshot buffers
+    void **peer_quat_dev = nullptr;       // box worlds: [2][P] each rank's orientation snapshots
     int64_t **peer_flags_dev = nullptr;   // [P] device array: each rank's flag array
     std::vector<void *> ipc_opened;       // peer mappings to close
     // recording
@@ -178,6 +193,10 @@ struct rb_world {
 
     int sp() const { return (int)(c % 2); }
 };
+
+extern "C" {
+static void fit_period(rb_world *w, const double *qpos, bool force = false);   // (below)
+}
 
 namespace {
 
@@ -292,6 +311,13 @@ int prime(rb_world *w, double dt = 0, double e = 0, double mu = 0) {
     return RB_OK;
 }
 
+// the per-step kernel form of this world (box worlds: no helper wave, the
+// box kernel shares its queue with the plain cooperative form)
+int step_form(const rb_world *w) {
+    return w->n_local <= w->coop_max ? (w->n_local <= w->help_max && !w->boxes ? FORM_COOP_HELP : FORM_COOP)
+           : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
+}
+
 int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, double mu, double thr) {
     hipError_t r;
     if (w->law == RB_LAW_BALLS) {
@@ -300,10 +326,10 @@ int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, doubl
         HIPCHK(r);
         return RB_OK;
     }
-    const int form = w->n_local <= w->coop_max ? (w->n_local <= w->help_max ? FORM_COOP_HELP : FORM_COOP)
-                     : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
-    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, form, w->boxes, s);
-    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, form, w->boxes, s);
+    const int form = step_form(w);
+    const bool boxes = w->boxes && w->box_kernel_on;
+    if (w->dtype == RB_F64) r = launch_step<double>(make_step<double>(w, c, dt, e, mu, thr, true), w->maxp, form, boxes, s);
+    else r = launch_step<float>(make_step<float>(w, c, dt, e, mu, thr, true), w->maxp, form, boxes, s);
     HIPCHK(r);
     return RB_OK;
 }
@@ -387,6 +413,10 @@ template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp) {
     pp.P = (int32_t)w->P;
     pp.S = w->S;
     pp.timeout_ticks = 500000000;      // 5 s at 100 MHz
+    if (w->boxes) {
+        pp.peer_quat = reinterpret_cast<const T *const *>(w->peer_quat_dev + (size_t)nsp * w->P);
+        pp.qdst = dp<T>(w->qsnap[nsp], 0);
+    }
     return pp;
 }
 
@@ -400,7 +430,7 @@ template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
     hp.push_cnt = w->push_cnt;
     hp.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
     hp.mail = reinterpret_cast<const char *>(w->flags);
-    hp.lay = MailLayout::make(w->P, w->S, w->esz);
+    hp.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
     hp.epoch = w->epoch;
     hp.rank = (int32_t)w->rank;
     hp.P = (int32_t)w->P;
@@ -408,7 +438,21 @@ template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
     hp.lo = w->lo;
     hp.S = w->S;
     hp.timeout_ticks = 500000000;      // 5 s at 100 MHz
+    hp.quat = w->boxes ? dp<T>(w->qsnap[nsp], 0) : nullptr;
     return hp;
+}
+
+// in-place all-gather of the snapshot of parity sp (and, box worlds, of the
+// orientation snapshot: [P][S][4] the same way)
+int rccl_gather(rb_world *w, int sp, hipStream_t s) {
+    const size_t n = (size_t)4 * w->S;
+    const ncclDataType_t ty = w->dtype == RB_F64 ? ncclFloat64 : ncclFloat32;
+    for (int k = 0; k < (w->boxes ? 2 : 1); ++k) {
+        char *buf = static_cast<char *>(k == 0 ? w->snap[sp] : w->qsnap[sp]);
+        const ncclResult_t r = rccl().AllGather(buf + (size_t)w->esz * n * w->rank, buf, n, ty, w->comm, s);
+        if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
+    }
+    return RB_OK;
 }
 
 // The in-library exchange after the step kernel of step c (which put the own
@@ -435,11 +479,7 @@ int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
         HIPCHK(pe);
         return RB_OK;
     }
-    char *buf = static_cast<char *>(w->snap[nsp]);
-    const size_t n = (size_t)4 * w->S;
-    const ncclResult_t r = rccl().AllGather(buf + (size_t)w->esz * n * w->rank, buf, n,
-                                            w->dtype == RB_F64 ? ncclFloat64 : ncclFloat32, w->comm, s);
-    if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
+    if (int rc = rccl_gather(w, nsp, s)) return rc;
     const hipError_t ie =
         w->dtype == RB_F64
             ? launch_insert<double>(make_insert<double>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local), s)
@@ -628,6 +668,98 @@ int tile_finish(rb_world *w) {
     return RB_OK;
 }
 
+// Guarded chunks (enqueue_steps): the chunk-start copy (state rows,
+// snapshot, box orientations, error word), the check after the chunk (error
+// word, deferral counts: one host sync), the roll-back.
+constexpr int64_t GUARD_MIN_STEPS = 64;   // shorter synchronous calls are not guarded (their
+                                          // save + check would cost a few % of the call)
+size_t chunk_save_bytes(const rb_world *w) {
+    return (size_t)w->esz * (13 * (size_t)w->S + 8 * (size_t)w->Npad) + sizeof(int32_t);
+}
+int chunk_save(rb_world *w) {
+    if (!w->opt_save) {
+        HIPCHK(hipMalloc(&w->opt_save, chunk_save_bytes(w)));
+        HIPCHK(hipHostMalloc((void **)&w->defer_host, sizeof(int32_t) * 3, 0));
+    }
+    char *o = static_cast<char *>(w->opt_save);
+    const size_t st = (size_t)w->esz * 13 * w->S, sn = (size_t)w->esz * 4 * w->Npad;
+    HIPCHK(hipMemcpyAsync(o, w->state, st, hipMemcpyDeviceToDevice, w->stream));
+    HIPCHK(hipMemcpyAsync(o + st, w->snap[w->sp()], sn, hipMemcpyDeviceToDevice, w->stream));
+    if (w->boxes) HIPCHK(hipMemcpyAsync(o + st + sn, w->qsnap[w->sp()], sn, hipMemcpyDeviceToDevice, w->stream));
+    HIPCHK(hipMemcpyAsync(o + st + 2 * sn, w->err, sizeof(int32_t), hipMemcpyDeviceToDevice, w->stream));
+    if (w->boxes) HIPCHK(hipMemsetAsync(w->defer_cnt, 0, sizeof(int32_t) * 2, w->stream));
+    return RB_OK;
+}
+int chunk_check(rb_world *w, int32_t &err, bool &deferred) {
+    HIPCHK(hipMemcpyAsync(w->defer_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+    if (w->boxes) HIPCHK(hipMemcpyAsync(w->defer_host + 1, w->defer_cnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    err = w->defer_host[0];
+    deferred = w->boxes && (w->defer_host[1] | w->defer_host[2]) != 0;
+    return RB_OK;
+}
+int chunk_restore(rb_world *w) {
+    const char *o = static_cast<const char *>(w->opt_save);
+    const size_t st = (size_t)w->esz * 13 * w->S, sn = (size_t)w->esz * 4 * w->Npad;
+    HIPCHK(hipMemcpyAsync(w->state, o, st, hipMemcpyDeviceToDevice, w->stream));
+    HIPCHK(hipMemcpyAsync(w->snap[w->sp()], o + st, sn, hipMemcpyDeviceToDevice, w->stream));
+    if (w->boxes) HIPCHK(hipMemcpyAsync(w->qsnap[w->sp()], o + st + sn, sn, hipMemcpyDeviceToDevice, w->stream));
+    HIPCHK(hipMemcpyAsync(w->err, o + st + 2 * sn, sizeof(int32_t), hipMemcpyDeviceToDevice, w->stream));
+    if (w->boxes) HIPCHK(hipMemsetAsync(w->defer_cnt, 0, sizeof(int32_t) * 2, w->stream));
+    w->primed = false;
+    return RB_OK;
+}
+// twice the buckets (both tables, emptied), if under the world's limit; the
+// linear layout's period gets the extra bit (refit_from_device re-splits it)
+int grow_table(rb_world *w, bool &grown) {
+    grown = false;
+    if (w->H * 2 > w->hmax) return RB_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);                                   // H and the grid are captured kernel arguments
+    const int64_t H = w->H * 2;
+    for (int k = 0; k < 2; ++k) {
+        HIPCHK(hipFree(w->ids[k]));
+        w->ids[k] = nullptr;
+        HIPCHK(hipMalloc((void **)&w->ids[k], sizeof(uint32_t) * LINE_WORDS * H));
+        HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * H));
+        if (w->pos[k]) {
+            HIPCHK(hipFree(w->pos[k]));
+            w->pos[k] = nullptr;
+            HIPCHK(hipMalloc(&w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * H));
+        }
+    }
+    w->H = H;
+    if ((w->group >> 24) & 1) {
+        const int lx = (w->group >> 12) & 15, ly = (w->group >> 16) & 15;
+        w->group += lx < 15 ? (1 << 12) : ly < 15 ? (1 << 16) : (1 << 20);
+    }
+    w->fit_valid = false;
+    w->primed = false;
+    w->table_grows += 1;
+    grown = true;
+    return RB_OK;
+}
+
+// the layout period refitted to the current positions (the snapshot)
+int refit_from_device(rb_world *w) {
+    std::vector<double> q((size_t)7 * w->N, 0.0);
+    if (w->dtype == RB_F64) {
+        std::vector<double> sn((size_t)4 * w->N);
+        HIPCHK(hipMemcpyAsync(sn.data(), w->snap[w->sp()], sizeof(double) * sn.size(), hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        for (int64_t b = 0; b < w->N; ++b)
+            for (int d = 0; d < 3; ++d) q[(size_t)(7 * b + d)] = sn[(size_t)(4 * b + d)];
+    } else {
+        std::vector<float> sn((size_t)4 * w->N);
+        HIPCHK(hipMemcpyAsync(sn.data(), w->snap[w->sp()], sizeof(float) * sn.size(), hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        for (int64_t b = 0; b < w->N; ++b)
+            for (int d = 0; d < 3; ++d) q[(size_t)(7 * b + d)] = sn[(size_t)(4 * b + d)];
+    }
+    fit_period(w, q.data(), true);
+    return RB_OK;
+}
+
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded,
                   bool allow_tile) {
@@ -671,12 +803,8 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         ++w->c;
         return RB_OK;
     }
-    const int variant = (int)w->record | (sharded ? 2 : 0);
     // K > 1: replay a captured graph of K step nodes
-    const int64_t chunk_max = 512;
-    int64_t left = nsteps;
-    while (left > 0) {
-        const int64_t K = left > chunk_max ? chunk_max : left;
+    auto replay = [&](int64_t K, int variant) -> int {
         auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
         auto it = w->graphs.find(key);
         if (it == w->graphs.end()) {
@@ -705,6 +833,75 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         }
         it->second.used = ++w->graph_tick;
         HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
+        return RB_OK;
+    };
+    const int variant = (int)w->record | (sharded ? 2 : 0);
+    const int64_t chunk_max = 512;
+    int64_t left = nsteps;
+    while (left > 0) {
+        int64_t K = left > chunk_max ? chunk_max : left;
+        bool opt = w->boxes && w->box_opt && !sharded && w->P == 1 && w->box_skip == 0;
+        // a guarded chunk can be rolled back: optimistic box chunks, and long
+        // chunks of a synchronous call (rb_step), whose broadphase layout is
+        // refitted if the scene drifted out of it (a bucket overflowed)
+        const bool guard = opt || (w->sync_call && K >= GUARD_MIN_STEPS && !sharded && w->P == 1 &&
+                                   w->law == RB_LAW_MUJOCO);
+        if (!guard) {
+            if (w->box_skip > 0) --w->box_skip;
+            if (int rc = replay(K, variant)) return rc;
+            w->c += K;
+            left -= K;
+            continue;
+        }
+        bool refitted = false;
+        for (;;) {
+            if (int rc = chunk_save(w)) return rc;
+            w->box_kernel_on = !opt;
+            const int rc = replay(K, variant | (opt ? 4 : 0));
+            w->box_kernel_on = true;
+            if (rc) return rc;
+            int32_t err = 0;
+            bool deferred = false;
+            if (int rc2 = chunk_check(w, err, deferred)) return rc2;
+            if (opt) w->box_stats[0] += 1;
+            // bucket overflow right after a fit of one step: a real overflow
+            // (reported by the caller's error check)
+            const bool overflow = (err & ERR_BUCKET_OVERFLOW) && !(refitted && K == 1);
+            deferred = deferred && opt;
+            if (!overflow && !deferred) {
+                if (opt && w->box_backoff > 0) w->box_backoff /= 2;
+                break;
+            }
+            if (int rc3 = chunk_restore(w)) return rc3;
+            if (deferred) {
+                // a box-involved pair came into range: the chunk again, from
+                // its start, with the box kernel; the next chunks keep it
+                w->box_stats[1] += 1;
+                w->box_backoff = w->box_backoff ? std::min(2 * w->box_backoff, 64) : 1;
+                w->box_skip = w->box_backoff;
+                opt = false;
+            }
+            if (overflow) {
+                // the scene outgrew the layout it was fitted for: refit to
+                // the chunk-start positions; if the chunk overflows again,
+                // a table twice the size (one more period bit), and once the
+                // table is at its limit, shorter chunks
+                if (refitted) {
+                    bool grown = false;
+                    if (int rc3 = grow_table(w, grown)) return rc3;
+                    if (!grown) K = K > 1 ? K / 2 : 1;
+                }
+                if (int rc3 = refit_from_device(w)) return rc3;
+                w->refits += 1;
+                refitted = true;
+            }
+            // table headers only rise (atomicMax on generation): the
+            // replay's generations must lie above every one the rolled-
+            // back chunk used
+            w->gen_off += (uint32_t)K + 1u;
+            if (int rc3 = gen_guard(w, left + K)) return rc3;
+            if (int rc3 = prime(w, dt, e, mu)) return rc3;
+        }
         w->c += K;
         left -= K;
     }
@@ -800,14 +997,15 @@ void free_world(rb_world *w) {
     drop_graphs(w);
     if (w->comm) (void)rccl().CommDestroy(w->comm);
     for (void *q : w->ipc_opened) (void)hipIpcCloseMemHandle(q);
-    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_flags_dev, w->bounds, w->push_cnt};
+    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_quat_dev, w->peer_flags_dev, w->bounds, w->push_cnt};
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *tbufs[] = {w->tile_rec, w->tile_count, w->tile_ctl};
+    void *tbufs[] = {w->tile_rec, w->tile_count, w->tile_ctl, w->opt_save};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_ctl_host) (void)hipHostFree(w->tile_ctl_host);
+    if (w->defer_host) (void)hipHostFree(w->defer_host);
     void *bufs[] = {w->snap[0], w->snap[1], w->qsnap[0], w->qsnap[1], w->defer_q, w->defer_cnt, w->state, w->consts, w->kind, w->xfrc, w->gen,
                     w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
@@ -874,7 +1072,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     for (int64_t b = 0; b < d->n_bodies && !any_box; ++b) any_box = d->kind[b] != RB_BODY_SPHERE;
     // box-involved pairs are solved on unsharded worlds (a box partner's
     // orientation must be the step-start one; shards exchange positions only)
-    w->boxes = any_box && w->P == 1;
+    w->boxes = any_box;
     // records per body: 4 per plane, 1 per sphere partner, up to 4 per
     // partner in scenes with boxes (oracle/rb_oracle_impl.h contact_stride)
     w->maxrec = 4 * w->n_planes + (any_box ? 4 : 1) * w->maxp;
@@ -884,6 +1082,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // K-step tile blocks (rb_tile.hip): RBHIP_TILE = 0 off, 1 on, unset auto
     // (sphere worlds of >= RBHIP_TILE_MIN_BODIES on one rank)
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) ? 1 : 0;
+    if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_TILE_K")) w->tile_kmax = std::max(1, std::min(64, atoi(ev)));
     if (const char *ev = getenv("RBHIP_TILE_BAND")) w->tile_band = atof(ev);
     if (const char *ev = getenv("RBHIP_TILE_OWNED")) w->tile_owned = std::max<int64_t>(16, atoll(ev));
@@ -909,6 +1108,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     int64_t hmax = 4096;
     while (hmax * 2 * per_bucket <= cap_bytes && hmax < (int64_t(1) << 26)) hmax *= 2;
     w->H = next_pow2(want) < hmax ? next_pow2(want) : hmax;
+    w->hmax = hmax;
     // The one-lane and wide forms group cells 8x8x4, the buckets of a group
     // contiguous (32 KB of lines), and lay the groups out linearly, periodic
     // in 2^lx x 2^ly x 2^lz groups (below): against a hash per cell measured
@@ -1055,7 +1255,7 @@ int rb_set_stream(rb_world *w, void *s) {
 // layout and still fits 4M flat spheres (1.33 -> 0.87 ms) and 32k on a
 // 128 x 256 grid (17.9 -> 13.2 us).  Deterministic in the global positions,
 // so every rank of a sharded world picks the same split.
-static void fit_period(rb_world *w, const double *qpos) {
+static void fit_period(rb_world *w, const double *qpos, bool force) {
     if (!((w->group >> 24) & 1)) return;                 // hashed layouts have no period
     if (const char *ev = getenv("RBHIP_FIT_PERIOD"))
         if (atoi(ev) == 0) return;                       // diagnostic: keep the creation-time split
@@ -1095,7 +1295,7 @@ static void fit_period(rb_world *w, const double *qpos) {
             }
         const int64_t key[7] = {gb_lo[0], gb_lo[1], gb_lo[2], gb_hi[0], gb_hi[1], gb_hi[2], (int64_t)w->group};
         const char *ev = getenv("RBHIP_FIT_PERIOD");
-        if (w->fit_valid && memcmp(key, w->fit_key, sizeof key) == 0 && !(ev && atoi(ev) == 2)) return;
+        if (!force && w->fit_valid && memcmp(key, w->fit_key, sizeof key) == 0 && !(ev && atoi(ev) == 2)) return;
         memcpy(w->fit_key, key, sizeof key);
         w->fit_valid = true;
     }
@@ -1306,7 +1506,9 @@ int rb_sync(rb_world *w) {
 }
 
 int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    if (w) w->sync_call = true;
     int rc = rb_step_async(w, nsteps, dt, e, mu, thr);
+    if (w) w->sync_call = false;
     if (rc) return rc;
     if ((rc = tile_finish(w))) return rc;
     return read_err(w);
@@ -1345,6 +1547,14 @@ int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *e
     return RB_OK;
 }
 
+int rb_gquat_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (dev_ptr) *dev_ptr = w->boxes ? w->qsnap[1 - w->sp()] : nullptr;
+    if (shard_elems) *shard_elems = w->boxes ? 4 * w->S : 0;
+    if (elem_bytes) *elem_bytes = w->esz;
+    return RB_OK;
+}
+
 int rb_comm_unique_id(void *id, int32_t bytes) {
     if (!id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
     if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
@@ -1365,20 +1575,21 @@ int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
     ncclResult_t r = rccl().CommInitRank(&w->comm, (int)w->P, u, (int)w->rank);
     if (r != ncclSuccess) { w->comm = nullptr; return fail(RB_ENODEV, "ncclCommInitRank: %s", rccl().GetErrorString(r)); }
     // first collective outside any graph capture (connection setup); the
-    // snapshot is replicated, so the in-place gather leaves it unchanged
-    char *buf = static_cast<char *>(w->snap[w->sp()]);
-    const size_t n = (size_t)4 * w->S;
-    r = rccl().AllGather(buf + (size_t)w->esz * n * w->rank, buf, n, w->dtype == RB_F64 ? ncclFloat64 : ncclFloat32,
-                         w->comm, w->stream);
-    if (r != ncclSuccess) return fail(RB_ENODEV, "ncclAllGather: %s", rccl().GetErrorString(r));
+    // snapshots are replicated, so the in-place gather leaves them unchanged
+    if (int rc = rccl_gather(w, w->sp(), w->stream)) return rc;
     HIPCHK(hipStreamSynchronize(w->stream));
     drop_graphs(w);
     return RB_OK;
 }
 
+// IPC handles per rank: both snapshots, the mailbox, (box worlds) both
+// orientation snapshots
+int p2p_nhandles(const rb_world *w) { return w->boxes ? 5 : 3; }
+
 int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
     if (!w || !len) return fail(RB_EINVAL, "null argument");
-    const int64_t need = 3 * (int64_t)sizeof(hipIpcMemHandle_t);
+    const int nh = p2p_nhandles(w);
+    const int64_t need = nh * (int64_t)sizeof(hipIpcMemHandle_t);
     *len = need;
     if (!out) return RB_OK;
     if (cap < need) return fail(RB_EINVAL, "handle buffer needs %lld bytes", (long long)need);
@@ -1386,26 +1597,31 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
     if (!w->flags) {
         // the mailbox, uncached: peers write it over xGMI while this rank's
         // kernels poll and read it
-        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz);
+        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
         HIPCHK(hipExtMallocWithFlags((void **)&w->flags, (size_t)lay.bytes, hipDeviceMallocUncached));
         HIPCHK(hipMemset(w->flags, 0, (size_t)lay.bytes));
     }
-    hipIpcMemHandle_t h[3];
+    hipIpcMemHandle_t h[5];
     HIPCHK(hipIpcGetMemHandle(&h[0], w->snap[0]));
     HIPCHK(hipIpcGetMemHandle(&h[1], w->snap[1]));
     HIPCHK(hipIpcGetMemHandle(&h[2], w->flags));
-    memcpy(out, h, sizeof(h));
+    if (w->boxes) {
+        HIPCHK(hipIpcGetMemHandle(&h[3], w->qsnap[0]));
+        HIPCHK(hipIpcGetMemHandle(&h[4], w->qsnap[1]));
+    }
+    memcpy(out, h, need);
     return RB_OK;
 }
 
 int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     if (!w || !all) return fail(RB_EINVAL, "null argument");
-    const int64_t blob = 3 * (int64_t)sizeof(hipIpcMemHandle_t);
+    const int nh = p2p_nhandles(w);
+    const int64_t blob = nh * (int64_t)sizeof(hipIpcMemHandle_t);
     if (len != blob * w->P) return fail(RB_EINVAL, "expected %lld bytes of handles (P blobs)", (long long)(blob * w->P));
     if (!w->flags) return fail(RB_EINVAL, "rb_p2p_handles first");
     if (w->p2p) return fail(RB_EINVAL, "already connected");
     HIPCHK(hipSetDevice(w->device));
-    std::vector<void *> snaps(2 * (size_t)w->P, nullptr);
+    std::vector<void *> snaps(2 * (size_t)w->P, nullptr), quats(2 * (size_t)w->P, nullptr);
     std::vector<int64_t *> flags((size_t)w->P, nullptr);
     const char *b = static_cast<const char *>(all);
     for (int64_t q = 0; q < w->P; ++q) {
@@ -1413,12 +1629,14 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
             snaps[(size_t)q] = w->snap[0];
             snaps[(size_t)(w->P + q)] = w->snap[1];
             flags[(size_t)q] = w->flags;
+            quats[(size_t)q] = w->qsnap[0];
+            quats[(size_t)(w->P + q)] = w->qsnap[1];
             continue;
         }
-        hipIpcMemHandle_t h[3];
-        memcpy(h, b + blob * q, sizeof(h));
-        void *ptr[3] = {};
-        for (int k = 0; k < 3; ++k) {
+        hipIpcMemHandle_t h[5];
+        memcpy(h, b + blob * q, (size_t)blob);
+        void *ptr[5] = {};
+        for (int k = 0; k < nh; ++k) {
             if (hipIpcOpenMemHandle(&ptr[k], h[k], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
                 return fail(RB_ENODEV, "hipIpcOpenMemHandle(rank %lld, buffer %d) failed", (long long)q, k);
             w->ipc_opened.push_back(ptr[k]);
@@ -1426,6 +1644,12 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
         snaps[(size_t)q] = ptr[0];
         snaps[(size_t)(w->P + q)] = ptr[1];
         flags[(size_t)q] = static_cast<int64_t *>(ptr[2]);
+        quats[(size_t)q] = ptr[3];
+        quats[(size_t)(w->P + q)] = ptr[4];
+    }
+    if (w->boxes) {
+        HIPCHK(hipMalloc((void **)&w->peer_quat_dev, sizeof(void *) * quats.size()));
+        HIPCHK(hipMemcpy(w->peer_quat_dev, quats.data(), sizeof(void *) * quats.size(), hipMemcpyHostToDevice));
     }
     HIPCHK(hipMalloc((void **)&w->peer_snap_dev, sizeof(void *) * snaps.size()));
     HIPCHK(hipMalloc((void **)&w->peer_flags_dev, sizeof(int64_t *) * flags.size()));
@@ -1666,12 +1890,12 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = tile_finish(w)) return rc;
-    const int form = w->n_local <= w->coop_max ? (w->n_local <= w->help_max ? FORM_COOP_HELP : FORM_COOP)
-                     : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
+    const int form = step_form(w);
     const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), w->tile_stats[0], w->tile_stats[1], w->tile_stats[2],
                                        w->tile_stats[3], w->tile_stats[4], w->tile_stats[5], w->tile_stats[6],
                                        form, (int64_t)w->tile_ntx * w->tile_nty, w->tile_nt, w->tile_kmax, w->tile_cap,
-                                       (int64_t)(w->tile_size * 1e6), tile_eligible(w, 1 << 20) ? 1 : 0};
+                                       (int64_t)(w->tile_size * 1e6), tile_eligible(w, 1 << 20) ? 1 : 0,
+                                       w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

@@ -13,7 +13,8 @@ namespace rb {
 enum : int32_t {
     ERR_BUCKET_OVERFLOW = 1,    // broadphase bucket capacity exceeded
     ERR_PARTNER_OVERFLOW = 2,   // more sphere partners than max_partners
-    ERR_UNSUPPORTED = 4,        // box-involved body pair within bounding distance
+    ERR_UNSUPPORTED = 4,        // box-involved pair in range with no box kernel to take it (never raised
+                                // since box worlds, sharded or not, always launch one)
     ERR_DOMAIN = 8,             // non-finite / out-of-range position
     ERR_EXCHANGE = 16,          // peer-to-peer exchange: a peer's step did not arrive in time
 };
@@ -189,6 +190,10 @@ template <typename T> struct P2PParams {
     int32_t rank, P;
     int64_t S;
     int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) before ERR_EXCHANGE
+    // box worlds: each peer's orientation snapshot of this parity ([P], [Npad][4]),
+    // copied for the box bodies into the local one (else nullptr)
+    const T *const *peer_quat;
+    T *qdst;
 };
 
 // Halo exchange (rb_p2p.hip), for large shards: instead of reading every
@@ -209,18 +214,20 @@ constexpr int BOUND_STRIDE = 32;       // int32 per copy (128 B): min x y z, max
 //   int64  cnt[P]            halo: bodies peer q pushed, (e << 32) | count
 //   uint32 in_ids[P][S]      halo: pushed ids, region q written by peer q
 //   Snap   in_snap[P][S]     halo: their snapshots
+//   T      in_quat[P][S][4]  halo, box worlds: the orientations of pushed boxes
 // Packing the epoch into every word lets a reader tell a fresh word from a
 // stale one without a separate flag (and a release fence before it).
 struct MailLayout {
-    int64_t o_flags, o_box, o_cnt, o_ids, o_snap, bytes;
-    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz) {
+    int64_t o_flags, o_box, o_cnt, o_ids, o_snap, o_quat, bytes;   // o_quat: -1 without boxes
+    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz, bool boxes) {
         MailLayout m;
         m.o_flags = 0;
         m.o_box = 8 * P;
         m.o_cnt = m.o_box + 48 * P;
         m.o_ids = m.o_cnt + 8 * P;
         m.o_snap = (m.o_ids + 4 * P * S + 255) / 256 * 256;
-        m.bytes = m.o_snap + 4 * esz * P * S;
+        m.o_quat = boxes ? m.o_snap + 4 * esz * P * S : -1;
+        m.bytes = m.o_snap + (boxes ? 8 : 4) * esz * P * S;
         return m;
     }
 };
@@ -238,6 +245,9 @@ template <typename T> struct HaloParams {
     int32_t rank, P, n_local;
     int64_t lo, S;
     int64_t timeout_ticks;
+    // box worlds: the local orientation snapshot of the next step ([Npad][4];
+    // own boxes' rows fresh, pushed boxes' rows land here), else nullptr
+    T *quat;
 };
 
 // ---- K-step tile blocks (rb_tile.hip) ------------------------

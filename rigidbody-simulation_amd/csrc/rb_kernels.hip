@@ -114,8 +114,8 @@ __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Cont
 // sphere-sphere contact test, for a box-involved pair overlapping bounding
 // spheres (the narrowphase then decides; oracle gen_contacts does the
 // same).  Only the box kernel (BOXES) takes such a pair; the sphere step
-// kernels mark the body deferred to it (box worlds: p.defer_q) or, in
-// sharded worlds (box orientations are not exchanged), report it.
+// kernels mark the body deferred to it (box worlds, sharded or not: p.defer_q;
+// a sharded world's exchange carries the boxes' orientations).
 template <typename T, bool BOXES>
 __device__ __forceinline__ bool candidate_hit(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x, T rad, T bi,
                                               uint32_t tj, const Snap<T> &s, bool &defer) {
@@ -580,7 +580,10 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
     if (RB_ABLATE == 7) np_ = 0;                 // diagnostic: search, but solve no partner contact
     if (!active || k != 0 || RB_ABLATE == 4) return;
     if (!BOXES && defer) {                       // box worlds only (p.defer_q set)
-        p.defer_q[atomicAdd(p.defer_cnt, 1)] = l;
+        // queued for the box kernel; chunks replayed without it (rb_capi.hip
+        // box_opt) only count, and are rolled back if the count is not zero
+        const int32_t q = atomicAdd(p.defer_cnt, 1);
+        if (q < p.S) p.defer_q[q] = l;
         return;
     }
     if constexpr (!early) {
@@ -613,17 +616,11 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
                               help_planes);
 }
 
-// Halo exchange: fold the wave's new cells (cell[0] == INT32_MAX: none) into
-// the step's bound copies — one atomic min/max per axis per wave, on copy
-// (block % BOUND_COPIES).  Every lane of the wave must call it.
-__device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell) {
-    int32_t lo[3], hi[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const bool have = cell[0] != INT32_MAX;
-        lo[d] = have ? cell[d] : INT32_MAX;
-        hi[d] = have ? cell[d] : INT32_MIN;
-    }
+// Halo exchange: fold the wave's new cells, given as per-lane boxes
+// (lo[0] == INT32_MAX: none), into the step's bound copies — one atomic
+// min/max per axis per wave, on copy (block % BOUND_COPIES).  Every lane of
+// the wave must call it.
+__device__ __forceinline__ void fold_box(int32_t *bounds, int32_t lo[3], int32_t hi[3]) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
@@ -636,6 +633,17 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
 #pragma unroll
         for (int d = 0; d < 3; ++d) { atomicMin(c + d, lo[d]); atomicMax(c + 3 + d, hi[d]); }
     }
+}
+// one cell per lane (cell[0] == INT32_MAX: none)
+__device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell) {
+    int32_t lo[3], hi[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const bool have = cell[0] != INT32_MAX;
+        lo[d] = have ? cell[d] : INT32_MAX;
+        hi[d] = have ? cell[d] : INT32_MIN;
+    }
+    fold_box(bounds, lo, hi);
 }
 
 // Helper wave of the cooperative form (HELP): one lane per body of the
@@ -793,12 +801,19 @@ void box_kernel(StepParams<T> p) {
     const int tid = threadIdx.x;
     const uint32_t gen = *p.cur.gen;
     const int32_t n = *p.defer_cnt;
+    int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
     for (int64_t qi = (int64_t)blockIdx.x * STEP_BLOCK + tid; qi < n; qi += (int64_t)gridDim.x * STEP_BLOCK) {
         int32_t cell[3] = {INT32_MAX, 0, 0};
         // one lane per body: the lane's LDS column (partner list, polygon) is slot = tid
         body_step<T, MAXP, 1, false, true>(p, Lead<T>::of(p), true, p.defer_q[qi], tid, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
                                            cell, gen, s_poly);
+        if (cell[0] != INT32_MAX)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { lo[d] = min(lo[d], cell[d]); hi[d] = max(hi[d], cell[d]); }
     }
+    // halo exchange: the deferred bodies' new cells (the step kernel folded
+    // only the bodies it stepped itself)
+    if (p.bounds) fold_box(p.bounds, lo, hi);
     if (blockIdx.x == 0 && tid == 0) *p.defer_reset = 0;    // the next step's queue
 }
 // one wave per SIMD (up to 64 x 1024 owned bodies): every register is free

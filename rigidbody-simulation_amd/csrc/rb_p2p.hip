@@ -48,6 +48,12 @@ template <typename T> __device__ __forceinline__ void store_snap_sys(Snap<T> *p,
     __hip_atomic_store(w + 3, s.r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// a box's orientation row (w x y z) from another GPU's memory
+template <typename T> __device__ __forceinline__ void copy_quat_sys(T *dst, const T *src) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
     const int64_t e = *p.epoch;
@@ -76,7 +82,9 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
     if (id >= p.ins.count || (id >= p.ins.skip_lo && id < p.ins.skip_hi)) return;
     const Snap<T> s = load_snap_sys(p.peer_snap[id / p.S] + id);
     p.dst[id] = s;
-    insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, (uint32_t)id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u), *p.ins.tab.gen);
+    const bool box = p.ins.kind[id] != 0;
+    if (box && p.qdst) copy_quat_sys(p.qdst + 4 * id, p.peer_quat[id / p.S] + 4 * id);
+    insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, (uint32_t)id | (box ? BOX_FLAG : 0u), *p.ins.tab.gen);
 }
 
 // ---- halo exchange (large shards) -----------------------------------------
@@ -86,7 +94,8 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
 //           every block waits for all peers' bounds of step e, then each
 //           thread tests one own body's new cell against each peer's bounds
 //           +-1 cell and, if inside, appends (id, snapshot) to that peer's
-//           inbox (slot from a wave-aggregated atomic on push_cnt[peer]);
+//           inbox (slot from a wave-aggregated atomic on push_cnt[peer]),
+//           with a box's orientation in box worlds;
 //           each wave ends with a system-scope release (its remote stores
 //           complete before the kernel does);
 //   insert: block 0 stores push_cnt[q], epoch-tagged, into peer q's mailbox
@@ -176,10 +185,11 @@ __global__ __launch_bounds__(256) void halo_push_kernel(HaloParams<T> p) {
     const bool active = l < p.n_local;
     int32_t cx = 0, cy = 0, cz = 0;
     Snap<T> s{};
-    bool ok = false;
+    bool ok = false, box = false;
     if (active) {
         s = p.dst[p.lo + l];
         ok = cell_of(s.x, s.y, s.z, p.ins.grid.inv_cs, cx, cy, cz);   // else: ERR_DOMAIN raised by the step
+        box = p.quat && p.ins.kind[p.lo + l] != 0;
     }
     const uint64_t lt = (1ull << (tid & 63)) - 1ull;
     bool pushed = false;                          // wave-uniform
@@ -206,6 +216,12 @@ __global__ __launch_bounds__(256) void halo_push_kernel(HaloParams<T> p) {
                 Snap<T> *sn = reinterpret_cast<Snap<T> *>(mail + L.o_snap) + (int64_t)p.rank * p.S;
                 __hip_atomic_store(ids + slot, (uint32_t)(p.lo + l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 store_snap_sys(sn + slot, s);
+                if (box) {                        // a box: its orientation too
+                    T *qm = reinterpret_cast<T *>(mail + L.o_quat) + 4 * ((int64_t)p.rank * p.S + slot);
+                    const T *qs = p.quat + 4 * (p.lo + l);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) __hip_atomic_store(qm + k, qs[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
     }
@@ -257,7 +273,9 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
             continue;
         }
         p.dst[id] = s;
-        insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, id | (p.ins.kind[id] != 0 ? BOX_FLAG : 0u), gen);
+        const bool box = p.ins.kind[id] != 0;
+        if (box && p.quat) copy_quat_sys(p.quat + 4 * (int64_t)id, reinterpret_cast<const T *>(p.mail + L.o_quat) + 4 * o);
+        insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, id | (box ? BOX_FLAG : 0u), gen);
     }
 }
 

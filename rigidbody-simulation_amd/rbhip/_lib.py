@@ -56,6 +56,7 @@ SIGNATURES = {
     "rb_shard_step": (C.c_int, [_P, _D, _D, _D, _D]),
     "rb_shard_exchange_done": (C.c_int, [_P]),
     "rb_gpos_buffer": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(_I64), C.POINTER(_I32)]),
+    "rb_gquat_buffer": (C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(_I64), C.POINTER(_I32)]),
     "rb_comm_unique_id": (C.c_int, [_P, _I32]),
     "rb_shard_comm_init": (C.c_int, [_P, _P, _I32]),
     "rb_shard_run": (C.c_int, [_P, _I64, _D, _D, _D, _D]),
@@ -79,7 +80,8 @@ SIGNATURES = {
 # rb_world_stats indices (include/rbhip.h RB_STAT_*)
 STAT_NAMES = ["graphs", "tile_runs", "tile_blocks", "tile_redo_taint", "tile_redo_bound", "tile_restart",
               "tile_fallback", "tile_steps", "form", "tiles", "tile_threads", "tile_kmax", "tile_cap",
-              "tile_size_um", "tile_on"]
+              "tile_size_um", "tile_on", "box_opt_chunks", "box_rollbacks", "refits",
+              "table_grows", "buckets"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
               3: "rb::step_kernel_coop_help"}
 
@@ -94,6 +96,15 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"librbhip.so not built at {path}: run __graft_entry__.build() "
                            "(the HIP path has no CPU fallback)")
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64 /
+    # libhsa-runtime64 (same sonames as /opt/rocm's).  Loaded first, torch's
+    # copies also serve this library; loaded after ours, torch would bring a
+    # second HSA runtime that finds no GPU (torch.cuda.is_available() False,
+    # measured on MI355X), breaking torch interop (rbhip.shard buffers).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(L, name)

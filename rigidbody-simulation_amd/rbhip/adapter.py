@@ -195,17 +195,40 @@ def step_model(model, data, nsteps: int, dt: float, restitution: float, friction
     """Upload data's state, run nsteps reference steps on the GPU, write back
     (the free bodies' joints only, at their jnt_qposadr / jnt_dofadr)."""
     w = world_for(model, normal_convention, law, tol, restitution, friction)
-    qi, vi = state_index(model)
+    qi, vi, fb, contiguous = _layout(model, w)
     qpos, qvel = np.asarray(data.qpos), np.asarray(data.qvel)
-    w.set_state(qpos[qi], qvel[vi])
+    n = fb.shape[0]
+    contiguous = contiguous and all(isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous
+                                    for a in (data.qpos, data.qvel))
+    if contiguous:                  # free joints at qpos[0:7n] / qvel[0:6n]: views, no gathers
+        w.set_state(qpos[:7 * n].reshape(n, 7), qvel[:6 * n].reshape(n, 6))
+    else:
+        w.set_state(qpos[qi], qvel[vi])
     xf = np.asarray(getattr(data, "xfrc_applied", np.zeros((1, 6))))
-    fb = free_bodies(model)
-    xf_free = xf[fb] if xf.shape[0] > max(fb) else None
+    xf_free = xf[fb] if xf.shape[0] > fb[-1] else None
     w.set_xfrc(xf_free if xf_free is not None and np.any(xf_free) else None)
     w.step(nsteps, dt=dt, restitution=restitution, friction=friction, threshold=threshold)
-    q, v = w.get_state()
-    data.qpos[qi] = q
-    data.qvel[vi] = v
+    if contiguous:
+        w.get_state(data.qpos[:7 * n].reshape(n, 7), data.qvel[:6 * n].reshape(n, 6))
+    else:
+        q, v = w.get_state()
+        data.qpos[qi] = q
+        data.qvel[vi] = v
+
+
+def _layout(model, w: World):
+    """(qpos index, qvel index, free body ids, contiguous) of a model, cached
+    on its world: the per-frame entry pays no O(N) Python work for them
+    (65,536 bodies: 15.7 ms per call before, measured on MI355X)."""
+    lay = getattr(w, "_adapter_layout", None)
+    if lay is None:
+        qi, vi = state_index(model)
+        fb = np.asarray(free_bodies(model), dtype=np.int64)
+        n = fb.shape[0]
+        contiguous = (np.array_equal(qi, 7 * np.arange(n)[:, None] + np.arange(7)) and
+                      np.array_equal(vi, 6 * np.arange(n)[:, None] + np.arange(6)))
+        lay = w._adapter_layout = (qi, vi, fb, contiguous)
+    return lay
 
 
 def load_scene_model(scene: Scene):

@@ -2,7 +2,9 @@
 
 Rank r owns bodies [r*S, r*S + S), S = ceil(N / P).  The exchange buffer
 holds (x, y, z, bounding radius) per body in global id order ([P][S][4]);
-two such buffers alternate step by step inside the library.  Each step is Jacobi
+two such buffers alternate step by step inside the library.  Worlds with box
+bodies exchange a second [P][S][4] buffer, the orientations (w, x, y, z):
+a box's contacts depend on its orientation (rb_gquat_buffer).  Each step is Jacobi
 across bodies (multi_sphere_bounce.py:43-46: one contact pass, then every
 body updated from step-start data), and the reference treats a contact
 partner as static (collision.py:27), so a rank needs only the step-start
@@ -66,13 +68,25 @@ class _DeviceBuffer:
             "version": 2, "strides": None, "stream": None}
 
 
-def wrap_gpos(world: World, torch):
-    """Torch view of the buffer the pending exchange fills (call between
-    shard_step and shard_exchange_done)."""
-    ptr, shard_elems, esz = world.gpos_buffer()
+def _wrap(world: World, torch, which: str):
+    ptr, shard_elems, esz = getattr(world, which)()
+    if not ptr:
+        return None, 0
     total = shard_elems * world.world_size
     t = torch.as_tensor(_DeviceBuffer(ptr, total, esz), device=f"cuda:{torch.cuda.current_device()}")
     return t, shard_elems
+
+
+def wrap_gpos(world: World, torch):
+    """Torch view of the buffer the pending exchange fills (call between
+    shard_step and shard_exchange_done)."""
+    return _wrap(world, torch, "gpos_buffer")
+
+
+def wrap_gquat(world: World, torch):
+    """Torch view of the orientation buffer the pending exchange fills in
+    box worlds (None, 0 in sphere-only worlds)."""
+    return _wrap(world, torch, "gquat_buffer")
 
 
 class ShardedWorld:
@@ -176,30 +190,36 @@ class ShardedWorld:
         if self.P > 1:
             dist.barrier(group=self.group)   # every rank connected before any steps
 
-    def _buffer(self):
-        """(whole buffer, this rank's slice) of the pending exchange; the two
-        alternating buffers' views are built once."""
+    def _buffers(self):
+        """[(whole buffer, this rank's slice)] of the pending exchange: the
+        positions, and in box worlds the orientations; the alternating
+        buffers' views are built once."""
         if hasattr(self.world, "exchange_buffer"):
             buf, n = self.world.exchange_buffer(self.torch)
-            return buf, buf[self.rank * n:(self.rank + 1) * n]
-        ptr = self.world.gpos_buffer()[0]
-        v = self._views.get(ptr)
-        if v is None:
-            buf, n = wrap_gpos(self.world, self.torch)
-            v = self._views[ptr] = (buf, buf[self.rank * n:(self.rank + 1) * n])
-        return v
+            return [(buf, buf[self.rank * n:(self.rank + 1) * n])]
+        out = []
+        for which, wrap in (("gpos_buffer", wrap_gpos), ("gquat_buffer", wrap_gquat)):
+            ptr = getattr(self.world, which)()[0]
+            if not ptr:
+                continue
+            v = self._views.get(ptr)
+            if v is None:
+                buf, n = wrap(self.world, self.torch)
+                v = self._views[ptr] = (buf, buf[self.rank * n:(self.rank + 1) * n])
+            out.append(v)
+        return out
 
     def _exchange(self):
-        buf, mine = self._buffer()
-        n = mine.numel()
-        if self.transport == "nccl":
-            # in place: the input is this rank's chunk of the output buffer
-            self.dist.all_gather_into_tensor(buf, mine, group=self.group)
-        else:
-            cpu = mine.to("cpu")
-            out = self.torch.empty(self.P * n, dtype=cpu.dtype)
-            self.dist.all_gather_into_tensor(out, cpu, group=self.group)
-            buf.copy_(out.to(buf.device))
+        for buf, mine in self._buffers():
+            n = mine.numel()
+            if self.transport == "nccl":
+                # in place: the input is this rank's chunk of the output buffer
+                self.dist.all_gather_into_tensor(buf, mine, group=self.group)
+            else:
+                cpu = mine.to("cpu")
+                out = self.torch.empty(self.P * n, dtype=cpu.dtype)
+                self.dist.all_gather_into_tensor(out, cpu, group=self.group)
+                buf.copy_(out.to(buf.device))
 
     def step(self, nsteps: int = 1, **params):
         if self.transport in ("p2p", "rccl"):

@@ -145,6 +145,14 @@ class World:
         _lib.check(self._L.rb_gpos_buffer(self._h, C.byref(p), C.byref(n), C.byref(b)), "rb_gpos_buffer")
         return p.value, n.value, b.value
 
+    def gquat_buffer(self):
+        """(device pointer, elements per shard, bytes per element) of the
+        replicated [P][S][4] orientation buffer the same exchange fills in
+        box worlds; (None, 0, esz) for sphere-only worlds."""
+        p, n, b = C.c_void_p(), C.c_int64(), C.c_int32()
+        _lib.check(self._L.rb_gquat_buffer(self._h, C.byref(p), C.byref(n), C.byref(b)), "rb_gquat_buffer")
+        return p.value, n.value, b.value
+
     # ---- in-library exchange (RCCL communicator owned by the world) ---------
     @staticmethod
     def comm_unique_id() -> bytes:

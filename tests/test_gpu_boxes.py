@@ -94,7 +94,10 @@ def test_box_pile_bit_exact(rb, oracle, monkeypatch, form, env):
                 w.step(100)
             gq, gv = w.get_state()
             assert _same(gq, q) and _same(gv, v), f"state differs after step {t + 100}"
+        st = w.stats()
     assert {17, 32, 40} <= seen and (np.array(sorted(seen)) >= 1).any()
+    # chunks replayed without the box kernel were rolled back (bodies deferred)
+    assert st["box_opt_chunks"] >= 1 and st["box_rollbacks"] >= 1, st
 
 
 def test_box_pile_f32_bit_exact(rb, oracle):
@@ -149,3 +152,22 @@ def test_boxes_entering_range_bit_exact(rb, oracle, monkeypatch, form, env):
             assert _same(gq, q) and _same(gv, v), f"state differs at step {s}"
             kinds |= set(kin.tolist())
     assert {32, 40} <= kinds, kinds
+
+
+@pytest.mark.parametrize("optimistic", ["1", "0"])
+def test_boxes_entering_range_chunked(rb, oracle, monkeypatch, optimistic):
+    """The same scene in one 150-step call: replayed without the box kernel
+    (rb_world::box_opt), the chunk defers the cubes when they meet, is rolled
+    back to its start and replayed with the box kernel; bit-exact either way."""
+    monkeypatch.setenv("RBHIP_BOX_OPTIMISTIC", optimistic)
+    sc = _approaching_boxes()
+    q, v = oracle.step(oracle.OracleScene(sc, max_partners=32), sc.qpos0, sc.qvel0, 150)
+    with rb.World(sc, max_partners=32) as w:
+        w.step(150)
+        gq, gv = w.get_state()
+        st = w.stats()
+    assert _same(gq, q) and _same(gv, v)
+    if optimistic == "1":
+        assert st["box_opt_chunks"] == 1 and st["box_rollbacks"] == 1, st
+    else:
+        assert st["box_opt_chunks"] == 0, st

@@ -140,12 +140,14 @@ def test_c3_bench_windows_bit_exact(rb, oracle16):
     assert ss1 > 0 and ss2 > 1000, (ss1, ss2)
 
 
-@pytest.mark.parametrize("cfg,steps,every", [("c2", 2000, 500), ("c4", 400, 100), ("c5", 1000, 250)])
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg,steps,every", [("c2", 2000, 500), ("c4", 400, 100), ("c5", 2000, 500)])
 def test_config_long_run_bit_exact_vs_oracle(rb, oracle16, cfg, steps, every):
-    """C2 for the survey's 2,000 steps, C4 (65,536 spheres on the incline,
-    friction-dominated) for 400, C5 (16,384 cubes) for 1,000: state bit-exact
-    with the oracle at every checkpoint (graph-replayed chunks) and the last
-    step's contact lists bit-exact."""
+    """C2 and C5 (16,384 cubes) for the survey's 2,000 steps, C4 (65,536
+    spheres on the incline, friction-dominated) for 400: state bit-exact
+    with the oracle at every checkpoint (graph-replayed chunks; C5's replayed
+    without the box kernel, no cube pair ever in range) and the last step's
+    contact lists bit-exact."""
     from rbhip import scenes
     oracle = oracle16
     sc = scenes.make(cfg)
@@ -160,7 +162,30 @@ def test_config_long_run_bit_exact_vs_oracle(rb, oracle16, cfg, steps, every):
         q, v = oracle.step(osc, q, v, every - 1)
         w.step(every - 1)
         q, v, ss = _check_window(w, oracle, osc, q, v, steps, steps, cfg)
+        st = w.stats()
     assert ss > 0 or cfg != "c2"          # C2 exercises sphere-sphere contacts
+    if cfg == "c5":
+        assert st["box_opt_chunks"] >= 4 and st["box_rollbacks"] == 0, st
+
+
+@pytest.mark.timeout(900)
+def test_c4_drift_refits_layout_bit_exact(rb, oracle16):
+    """C4 for 2,000 steps: the spheres slide ~600 m down the incline and out
+    of the broadphase layout fitted at t = 0 (buckets overflow near step
+    1,000).  A synchronous rb_step rolls the chunk back, refits the layout
+    to the current positions and replays it — still bit-exact with the
+    oracle.  Sliding rows run into each other after ~550 steps (up to 28
+    sphere partners, measured with the oracle): max_partners = 32."""
+    from rbhip import scenes
+    sc = scenes.make("c4")
+    with rb.World(sc, max_partners=32) as w:
+        for _ in range(4):
+            w.step(500)
+        q, v = w.get_state()
+        st = w.stats()
+    q1, v1 = oracle16.step(oracle16.OracleScene(sc, max_partners=32), sc.qpos0, sc.qvel0, 2000)
+    assert _same(q, q1) and _same(v, v1)
+    assert st["refits"] >= 1, st
 
 
 def test_c3_one_step_parity_from_evolved_state(rb, oracle):
@@ -283,25 +308,33 @@ def test_graph_equals_single_launches_and_reruns(rb):
 
 
 @pytest.mark.parametrize("P,scene,steps", [(2, "flat800", 120), (3, "flat800", 120), (4, "flat800", 120),
-                                           (8, "c4", 240)])
+                                           (8, "c4", 240), (2, "boxpile", 400), (3, "boxpile", 400)])
 def test_shard_invariance_in_process(rb, P, scene, steps):
-    """P body-range shards on one device, positions exchanged by device copies
-    between their replicated buffers: bit-identical (uint64 words) to one
-    world, and the last step's contact lists equal.  (8, "c4") is BASELINE
-    configs[3] as the 8-GPU run shards it: 65,536 spheres on the incline,
-    8,192 per rank (the body loop of multi_sphere_bounce.py:46-90 split by
-    body-id range)."""
+    """P body-range shards on one device, positions (and in box worlds the
+    orientations) exchanged by device copies between their replicated
+    buffers: bit-identical (uint64 words) to one world, and the last step's
+    contact lists equal.  (8, "c4") is BASELINE configs[3] as the 8-GPU run
+    shards it: 65,536 spheres on the incline, 8,192 per rank (the body loop
+    of multi_sphere_bounce.py:46-90 split by body-id range).  "boxpile":
+    cube columns with sphere caps, shards meeting along a row of columns
+    (box-box, edge and sphere-box contacts across the seam)."""
     import torch
     from rbhip import scenes
-    from rbhip.shard import wrap_gpos
-    sc = scenes.flat_spheres(32, 25, seed=7) if scene == "flat800" else scenes.make(scene)   # 800: not a multiple of 3
-    with rb.World(sc) as ref:
+    from rbhip.shard import wrap_gpos, wrap_gquat
+    kw = {}
+    if scene == "flat800":
+        sc = scenes.flat_spheres(32, 25, seed=7)       # 800: not a multiple of 3
+    elif scene == "boxpile":
+        sc, kw = scenes.box_pile(6, 6, 3, seed=0), {"max_partners": 32}
+    else:
+        sc = scenes.make(scene)
+    with rb.World(sc, **kw) as ref:
         ref.step(steps - 1)
         ref.record_contacts(True)
         ref.step(1)
         rq, rv = ref.get_state()
         rc, rp, rk, rd = ref.contacts()
-    worlds = [rb.World(sc, rank=r, world_size=P) for r in range(P)]
+    worlds = [rb.World(sc, rank=r, world_size=P, **kw) for r in range(P)]
     for s in range(steps):
         if s == steps - 1:
             for w in worlds:
@@ -310,12 +343,15 @@ def test_shard_invariance_in_process(rb, P, scene, steps):
             w.shard_step()
         for w in worlds:
             w.sync()
-        bufs = [wrap_gpos(w, torch) for w in worlds]      # the buffers alternate per step
-        n = bufs[0][1]
-        for r, (buf, _) in enumerate(bufs):
-            for o, (obuf, _) in enumerate(bufs):
-                if o != r:
-                    buf[o * n:(o + 1) * n].copy_(obuf[o * n:(o + 1) * n])
+        for wrap in (wrap_gpos, wrap_gquat):
+            bufs = [wrap(w, torch) for w in worlds]      # the buffers alternate per step
+            n = bufs[0][1]
+            if bufs[0][0] is None:                       # sphere worlds: no orientations
+                continue
+            for r, (buf, _) in enumerate(bufs):
+                for o, (obuf, _) in enumerate(bufs):
+                    if o != r:
+                        buf[o * n:(o + 1) * n].copy_(obuf[o * n:(o + 1) * n])
         torch.cuda.synchronize()
         for w in worlds:
             w.shard_exchange_done()

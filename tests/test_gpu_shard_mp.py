@@ -21,12 +21,19 @@ def _free_port():
 
 
 def _scene(P, patch):
+    """(scene, World keywords, steps).  patch == "c4": BASELINE configs[3]
+    split by body-id range (strong scaling); "boxpile": tilted cube columns
+    with sphere caps (ids column by column, so the shards meet along a row of
+    columns: box-box, sphere-box and edge contacts across the seam)."""
     from rbhip import scenes
-    # patch == "c4": BASELINE configs[3] split by body-id range (strong scaling)
-    return scenes.make("c4") if patch == "c4" else scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2)
+    if patch == "c4":
+        return scenes.make("c4"), {}, 80
+    if patch == "boxpile":
+        return scenes.box_pile(6, 6, 3, seed=0), {"max_partners": 32}, 300
+    return scenes.tiled(scenes.flat_spheres, P, patch, patch, seed=2), {}, 80
 
 
-def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
+def _worker(rank, P, port, out, transport="host", halo=False, patch=16):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
@@ -34,8 +41,8 @@ def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=P)
     from rbhip.shard import ShardedWorld
-    sc = _scene(P, patch)
-    sw = ShardedWorld(sc, device=0, transport=transport, halo=halo)
+    sc, kw, steps = _scene(P, patch)
+    sw = ShardedWorld(sc, device=0, transport=transport, halo=halo, **kw)
     assert sw.transport == transport and sw.halo == halo
     sw.step(steps)
     sw.sync()
@@ -49,22 +56,24 @@ def _worker(rank, P, port, steps, out, transport="host", halo=False, patch=16):
 @pytest.mark.parametrize("P,transport,halo,patch", [(2, "host", False, 16), (2, "p2p", False, 16),
                                                     (3, "p2p", False, 16), (2, "p2p", True, 16),
                                                     (3, "p2p", True, 16), (2, "p2p", True, 96),
-                                                    (2, "p2p", True, "c4"), (2, "p2p", False, "c4")])
+                                                    (2, "p2p", True, "c4"), (2, "p2p", False, "c4"),
+                                                    (2, "host", False, "boxpile"), (2, "p2p", False, "boxpile"),
+                                                    (2, "p2p", True, "boxpile"), (3, "p2p", True, "boxpile")])
 def test_two_process_shards_match_single_world(tmp_path, P, transport, halo, patch):
     """Several processes on one GPU; "p2p" maps the other processes' buffers
     through IPC and synchronises on device flags, as across GPUs; halo=True
     pushes only the bodies within a cell of each peer's bounds (96x96
-    patches: 36 push blocks per rank, a wave-aggregated inbox per peer)."""
+    patches: 36 push blocks per rank, a wave-aggregated inbox per peer).
+    The box piles exchange the boxes' orientations with their positions
+    (full reads, halo pushes, host all-gather)."""
     import torch.multiprocessing as mp
     import rbhip
-    from rbhip import scenes
-    steps = 80
-    sc = _scene(P, patch)
-    with rbhip.World(sc) as w:
+    sc, kw, steps = _scene(P, patch)
+    with rbhip.World(sc, **kw) as w:
         w.step(steps)
         q1, v1 = w.get_state()
     out = str(tmp_path / "state.npy")
-    mp.start_processes(_worker, args=(P, _free_port(), steps, out, transport, halo, patch), nprocs=P,
+    mp.start_processes(_worker, args=(P, _free_port(), out, transport, halo, patch), nprocs=P,
                        start_method="spawn")
     got = np.load(out)
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
@@ -77,14 +86,16 @@ def test_two_process_shards_match_single_world(tmp_path, P, transport, halo, pat
 # remote insert is real).  The multi-rank data path is the same three
 # operations as the host-staged test above.
 
-def test_inlibrary_exchange_one_rank_matches_world():
+@pytest.mark.parametrize("scene", ["flat", "boxpile"])
+def test_inlibrary_exchange_one_rank_matches_world(scene):
     import rbhip
     from rbhip import scenes
-    sc = scenes.flat_spheres(24, 24, seed=5)
-    with rbhip.World(sc) as ref:
+    sc, kw = ((scenes.flat_spheres(24, 24, seed=5), {}) if scene == "flat" else
+              (scenes.box_pile(4, 4, 3, seed=1), {"max_partners": 32}))   # box pile: orientations gathered too
+    with rbhip.World(sc, **kw) as ref:
         ref.step(613)
         q1, v1 = ref.get_state()
-    with rbhip.World(sc) as w:
+    with rbhip.World(sc, **kw) as w:
         w.shard_comm_init(rbhip.World.comm_unique_id())
         for n in (1, 12, 600):              # eager, one graph, a 512 + 88 chunked replay
             w.shard_run(n)
