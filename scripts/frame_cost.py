@@ -8,9 +8,10 @@
    per call and split into set_state / step / get_state, on the scene's
    65,536 bodies, with the positions moving between calls (fit_period's
    group-box cache) and with the same positions.
-2. C4 drift: the wall clock of 200 steps at steps 261-460
-   and at 1,801-2,000 of one world (the layout period is fitted once, from
-   the initial positions).
+2. Drift: the wall clock of step windows of one world, the
+   layout fitted once from the initial positions: C4 (201-350, 451-600:
+   later windows overflow a bucket, see drift()) and C3 translating across
+   its layout (261-460, 1,801-2,000).
 One JSON line per measurement.
 """
 from __future__ import annotations
@@ -60,26 +61,45 @@ def frame_cost(cfg: str, frames: int):
                       **{f"{k}_ms_median": 1e3 * float(np.median(v)) for k, v in parts.items()}}), flush=True)
 
 
-def c4_drift():
-    # C4 needs max_partners >= 28 after ~550 steps (sliding rows run into
-    # each other: up to 28 sphere partners, the oracle with max_partners=64)
-    sc = scenes.make("c4")
+def window_times(sc, windows, **kw):
+    """Wall clock per step of each (first, last) step window of one world
+    (windows of one length, ascending; the graph of that length captured by
+    an untimed first call)."""
     out = {}
-    with rbhip.World(sc, max_partners=32) as w:
-        w.step(260)
-        w.step(200)                                  # graph capture outside the timed windows
-        w.step(1)
-        w.sync()
-        c = 461
-        for lo in (461, 1801):
-            w.step(lo - c)
+    n = windows[0][1] - windows[0][0] + 1
+    with rbhip.World(sc, **kw) as w:
+        w.step(n)
+        c = n
+        for lo, hi in windows:
+            assert hi - lo + 1 == n and lo - 1 >= c
+            if lo - 1 > c:
+                w.step(lo - 1 - c)
             w.sync()
-            t, _ = timed(lambda: w.step(200))
-            out[f"steps_{lo}_{lo + 199}_us_per_step"] = t / 200 * 1e6
-            c = lo + 200
-    a, b = out["steps_461_660_us_per_step"], out["steps_1801_2000_us_per_step"]
-    print(json.dumps({"what": "C4 drift: wall clock per step of 200-step windows (one world, max_partners 32)", **out,
-                      "late_over_early": b / a}), flush=True)
+            t, _ = timed(lambda: w.step(n))
+            out[f"steps_{lo}_{hi}_us_per_step"] = t / n * 1e6
+            c = hi
+    return out
+
+
+def drift():
+    # C4: rows sliding down the incline pile into each other after ~550
+    # steps (up to 28 sphere partners; 29 bodies in one cell at step 700,
+    # one short of a bucket's 30: later steps overflow it) -> windows before
+    # that, max_partners 32
+    sc = scenes.make("c4")
+    out = window_times(sc, [(201, 350), (451, 600)], max_partners=32)
+    print(json.dumps({"what": "C4: wall clock per step of step windows (one world, max_partners 32)", **out}),
+          flush=True)
+    # C3 translating at (10, 5) m/s: 200 m across its fitted layout by step 2,000
+    sc = scenes.make("c3")
+    qv = sc.qvel0.copy()
+    qv[:, 0] += 10.0
+    qv[:, 1] += 5.0
+    sc = sc.with_(qvel0=qv)
+    out = window_times(sc, [(261, 460), (1801, 2000)])
+    a, b = out["steps_261_460_us_per_step"], out["steps_1801_2000_us_per_step"]
+    print(json.dumps({"what": "C3 translating at (10, 5) m/s: wall clock per step of step windows (one world)",
+                      **out, "late_over_early": b / a}), flush=True)
 
 
 def main():
@@ -90,7 +110,7 @@ def main():
     a = ap.parse_args()
     frame_cost(a.config, a.frames)
     if not a.skip_drift:
-        c4_drift()
+        drift()
 
 
 if __name__ == "__main__":

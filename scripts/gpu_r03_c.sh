@@ -8,8 +8,8 @@ mkdir -p $OUT
 step() { echo "== $*  ($(date +%T))"; }
 step pytest
 timeout -k 10 1100 python -u -m pytest -x -v --timeout 900 --timeout-method thread tests/test_gpu_boxes.py \
-    "tests/test_gpu_parity.py::test_c4_drift_refits_layout_bit_exact" \
-    "tests/test_gpu_parity.py::test_config_long_run_bit_exact_vs_oracle" > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+    "tests/test_gpu_parity.py::test_bucket_overflow_rolls_back_and_refits_bit_exact" \
+    "tests/test_gpu_parity.py::test_config_long_run_bit_exact_vs_oracle[c5-2000-500]" > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 step frame-cost
 timeout -k 10 600 python scripts/frame_cost.py > $OUT/frame_cost.json 2> $OUT/frame_cost.err || { tail -5 $OUT/frame_cost.err; exit 1; }
