@@ -83,7 +83,7 @@ typedef struct rb_scene_desc {
     int32_t device;            /* HIP device ordinal                                   */
     int32_t rank;              /* shard index: owns bodies [rank*S, rank*S+S) ∩ [0,N)  */
     int32_t world_size;        /* shard count P; S = ceil(N / P)                       */
-    int32_t max_partners;      /* sphere-sphere contacts per body (0 = default 16)     */
+    int32_t max_partners;      /* sphere-sphere contacts per body (0 = default 16; a guarded rb_step chunk raises 16 to 32 on overflow) */
     int32_t bucket_capacity;   /* reserved (0): a broadphase bucket holds 30 ids       */
     const int32_t *kind;       /* [N]   RB_BODY_*                                      */
     const double  *mass;       /* [N]   model.body_mass of each free body              */
@@ -314,7 +314,8 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 #define RB_STAT_REFITS       17   /* broadphase layout refits of a drifting scene (chunk rolled back, replayed) */
 #define RB_STAT_TABLE_GROWS  18   /* of which with the bucket table doubled */
 #define RB_STAT_BUCKETS      19   /* buckets per table now */
-#define RB_STATS_COUNT       20
+#define RB_STAT_MAX_PARTNERS 20   /* max_partners now (16 -> 32 after an overflow in a guarded chunk) */
+#define RB_STATS_COUNT       21
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

@@ -124,12 +124,16 @@ struct rb_world {
     bool sync_call = false;        // inside rb_step (synchronous): long chunks are guarded
     int64_t refits = 0;            // layout refits after a bucket overflow (rolled back, replayed)
     int64_t table_grows = 0;       // of which with the table doubled
+    int64_t partner_grows = 0;     // max_partners raised 16 -> 32 after a partner overflow
+    int32_t diag_overflow = 0;     // RBHIP_DIAG_OVERFLOW=n (tests): the next n guarded chunk checks
+                                   // report a bucket overflow (the roll-back / refit / growth path)
     void *state = nullptr;     // 13 x S  (qw qx qy qz vx vy vz wx wy wz px py pz)
     void *vel[2] = {};         // two-ball law: [Npad] Vel<T>, ping-pong with the snapshots
     void *consts = nullptr;    // 8 x Npad (mass ix iy iz sx sy sz bound)
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
     uint32_t *ids[2] = {};     // [H][LINE_WORDS] bucket blocks (rb_internal.hpp Table; alternate with the snapshots)
+    uint32_t *spill[2] = {};   // [2 + 2 x SPILL_CAP] ids past full buckets, per table
     void *pos[2] = {};         // [H][LINE_WORDS] Snap<T> bucket slot snapshots
     uint32_t *gen = nullptr;   // [2] generation of the table of each step parity (rb_internal.hpp Table)
     uint32_t gen_off = 1;      // generation of step c's table = gen_off + c (host bookkeeping; only grows)
@@ -213,7 +217,7 @@ template <typename T> Grid<T> make_grid(const rb_world *w) {
 
 // the broadphase of the steps of parity sp
 template <typename T> Table<T> table(const rb_world *w, int sp) {
-    return Table<T>{w->ids[sp], w->pos[sp] ? dp<Snap<T>>(w->pos[sp], 0) : nullptr, w->gen + sp};
+    return Table<T>{w->ids[sp], w->pos[sp] ? dp<Snap<T>>(w->pos[sp], 0) : nullptr, w->gen + sp, w->spill[sp]};
 }
 
 // parameters of the step with counter value c
@@ -241,7 +245,7 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.snap_cur = dp<Snap<T>>(w->snap[sp], 0);
     p.snap_next = dp<Snap<T>>(w->snap[1 - sp], 0);
     p.cur = table<T>(w, sp);
-    p.next = insert_next ? table<T>(w, 1 - sp) : Table<T>{nullptr, nullptr, nullptr};
+    p.next = insert_next ? table<T>(w, 1 - sp) : Table<T>{nullptr, nullptr, nullptr, nullptr};
     p.err = w->err;
     p.epoch = w->p2p ? w->epoch : nullptr;
     p.bounds = w->halo ? w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE : nullptr;
@@ -311,10 +315,9 @@ int prime(rb_world *w, double dt = 0, double e = 0, double mu = 0) {
     return RB_OK;
 }
 
-// the per-step kernel form of this world (box worlds: no helper wave, the
-// box kernel shares its queue with the plain cooperative form)
+// the per-step kernel form of this world
 int step_form(const rb_world *w) {
-    return w->n_local <= w->coop_max ? (w->n_local <= w->help_max && !w->boxes ? FORM_COOP_HELP : FORM_COOP)
+    return w->n_local <= w->coop_max ? (w->n_local <= w->help_max ? FORM_COOP_HELP : FORM_COOP)
            : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
 }
 
@@ -522,7 +525,10 @@ int gen_guard(rb_world *w, int64_t nsteps) {
         return fail(RB_EOVERFLOW, "table generations exhausted after ~4e9 steps of a halo-exchanging shard: "
                                   "the sharded world must be recreated");
     HIPCHK(hipStreamSynchronize(w->stream));
-    for (int k = 0; k < 2; ++k) HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
+    for (int k = 0; k < 2; ++k) {
+        HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
+        HIPCHK(hipMemset(w->spill[k], 0, sizeof(uint32_t) * 2));
+    }
     w->gen_off = 1u - (uint32_t)w->c;   // prime() makes step c's generation 2
     w->primed = false;
     return RB_OK;
@@ -695,6 +701,7 @@ int chunk_check(rb_world *w, int32_t &err, bool &deferred) {
     if (w->boxes) HIPCHK(hipMemcpyAsync(w->defer_host + 1, w->defer_cnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
     err = w->defer_host[0];
+    if (w->diag_overflow > 0) { --w->diag_overflow; err |= ERR_BUCKET_OVERFLOW; }
     deferred = w->boxes && (w->defer_host[1] | w->defer_host[2]) != 0;
     return RB_OK;
 }
@@ -737,6 +744,26 @@ int grow_table(rb_world *w, bool &grown) {
     w->primed = false;
     w->table_grows += 1;
     grown = true;
+    return RB_OK;
+}
+
+// max_partners raised to 32 (the second kernel instantiation), contact
+// records resized to match
+int grow_partners(rb_world *w) {
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);                                   // the instantiation is chosen at capture
+    w->maxp = 32;
+    w->maxrec = 4 * w->n_planes + (w->boxes ? 4 : 1) * w->maxp;
+    if (w->rec_count) {
+        const size_t slots = (size_t)w->maxrec * (w->S > 0 ? w->S : 1);
+        void *old[] = {w->rec_partner, w->rec_kind, w->rec_dist};
+        for (void *b : old) HIPCHK(hipFree(b));
+        w->rec_partner = nullptr; w->rec_kind = nullptr; w->rec_dist = nullptr;
+        HIPCHK(hipMalloc((void **)&w->rec_partner, sizeof(int32_t) * slots));
+        HIPCHK(hipMalloc((void **)&w->rec_kind, sizeof(int32_t) * slots));
+        HIPCHK(hipMalloc(&w->rec_dist, (size_t)w->esz * slots));
+    }
+    w->partner_grows += 1;
     return RB_OK;
 }
 
@@ -867,8 +894,10 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
             // bucket overflow right after a fit of one step: a real overflow
             // (reported by the caller's error check)
             const bool overflow = (err & ERR_BUCKET_OVERFLOW) && !(refitted && K == 1);
+            // more sphere partners than max_partners 16: the 32-partner kernels
+            const bool partners = (err & ERR_PARTNER_OVERFLOW) && w->maxp < 32;
             deferred = deferred && opt;
-            if (!overflow && !deferred) {
+            if (!overflow && !deferred && !partners) {
                 if (opt && w->box_backoff > 0) w->box_backoff /= 2;
                 break;
             }
@@ -881,6 +910,8 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
                 w->box_skip = w->box_backoff;
                 opt = false;
             }
+            if (partners)
+                if (int rc3 = grow_partners(w)) return rc3;
             if (overflow) {
                 // the scene outgrew the layout it was fitted for: refit to
                 // the chunk-start positions; if the chunk overflows again,
@@ -1007,7 +1038,7 @@ void free_world(rb_world *w) {
     if (w->tile_ctl_host) (void)hipHostFree(w->tile_ctl_host);
     if (w->defer_host) (void)hipHostFree(w->defer_host);
     void *bufs[] = {w->snap[0], w->snap[1], w->qsnap[0], w->qsnap[1], w->defer_q, w->defer_cnt, w->state, w->consts, w->kind, w->xfrc, w->gen,
-                    w->ids[0], w->ids[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
+                    w->ids[0], w->ids[1], w->spill[0], w->spill[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -1070,8 +1101,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     w->maxp = maxp;
     bool any_box = false;
     for (int64_t b = 0; b < d->n_bodies && !any_box; ++b) any_box = d->kind[b] != RB_BODY_SPHERE;
-    // box-involved pairs are solved on unsharded worlds (a box partner's
-    // orientation must be the step-start one; shards exchange positions only)
+    // box-capable kernels (sharded worlds exchange the boxes' orientations)
     w->boxes = any_box;
     // records per body: 4 per plane, 1 per sphere partner, up to 4 per
     // partner in scenes with boxes (oracle/rb_oracle_impl.h contact_stride)
@@ -1083,6 +1113,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // (sphere worlds of >= RBHIP_TILE_MIN_BODIES on one rank)
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
+    if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     if (const char *ev = getenv("RBHIP_TILE_K")) w->tile_kmax = std::max(1, std::min(64, atoi(ev)));
     if (const char *ev = getenv("RBHIP_TILE_BAND")) w->tile_band = atof(ev);
     if (const char *ev = getenv("RBHIP_TILE_OWNED")) w->tile_owned = std::max<int64_t>(16, atoll(ev));
@@ -1196,6 +1227,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     }
     for (int k = 0; k < 2; ++k) {
         ALLOC(w->ids[k], sizeof(uint32_t) * LINE_WORDS * w->H);
+        ALLOC(w->spill[k], sizeof(uint32_t) * (2 + 2 * SPILL_CAP));
         // slot snapshots feed the cooperative search only
         if (needs_slot_snapshots(coop, split)) ALLOC(w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H);
     }
@@ -1212,6 +1244,8 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         // bucket headers of generation 0: every table's generation is >= 2
         hipMemset(w->ids[0], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
         hipMemset(w->ids[1], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
+        hipMemset(w->spill[0], 0, sizeof(uint32_t) * 2) != hipSuccess ||
+        hipMemset(w->spill[1], 0, sizeof(uint32_t) * 2) != hipSuccess ||
         hipMemset(w->gen, 0, sizeof(uint32_t) * 2) != hipSuccess ||
         hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipMemset failed"));
@@ -1895,7 +1929,8 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
                                        w->tile_stats[3], w->tile_stats[4], w->tile_stats[5], w->tile_stats[6],
                                        form, (int64_t)w->tile_ntx * w->tile_nty, w->tile_nt, w->tile_kmax, w->tile_cap,
                                        (int64_t)(w->tile_size * 1e6), tile_eligible(w, 1 << 20) ? 1 : 0,
-                                       w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H};
+                                       w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H,
+                                       (int64_t)w->maxp};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

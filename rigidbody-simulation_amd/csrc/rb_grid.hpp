@@ -231,6 +231,44 @@ __device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &ta
     }
     return {b, in ? 1 : 0, old, gen, RL >= 0 ? RL : grid_rl(g.super)};
 }
+// An id past a full bucket: appended (bucket, id) to the table's spill list,
+// claimed like a slot (generation-tagged count, atomicMax then atomicAdd)
+template <typename T>
+__device__ __forceinline__ void spill_insert(const Table<T> &tab, int32_t *err, uint32_t b, uint32_t tagged_id,
+                                          uint32_t gen) {
+    if (!tab.spill) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    auto *h = reinterpret_cast<unsigned long long *>(tab.spill);
+    atomicMax(h, (unsigned long long)gen << 32);
+    const unsigned long long old = atomicAdd(h, 1ull);
+    const uint32_t k = (uint32_t)(old >> 32) == gen ? (uint32_t)old : (uint32_t)SPILL_CAP;
+    if (k >= (uint32_t)SPILL_CAP) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    uint32_t *e = tab.spill + 2 + 2 * (int64_t)k;
+    wt_store(e, b);
+    wt_store(e + 1, tagged_id);
+}
+// f(tagged id) for each spilled id of bucket b (buckets whose header count
+// passed BUCKET_SLOTS only: the rare path, kept compact)
+template <typename T, typename F>
+__device__ __forceinline__ void spill_scan(const Table<T> &tab, uint32_t gen, uint32_t b, F f) {
+    if (!tab.spill) return;
+    const uint2 h = *reinterpret_cast<const uint2 *>(tab.spill);
+    const int32_t n = h.y != gen ? 0 : h.x < (uint32_t)SPILL_CAP ? (int32_t)h.x : SPILL_CAP;
+    const uint2 *e = reinterpret_cast<const uint2 *>(tab.spill + 2);
+#pragma unroll 1
+    for (int32_t k = 0; k < n; ++k) {
+        const uint2 v = e[k];
+        if (v.x == b) f(v.y);
+    }
+}
+// the header's count passed the slots: bucket b has spilled ids
+// (diagnostic builds RB_SPILL=0: searches ignore the spill list)
+#ifndef RB_SPILL
+#define RB_SPILL 1
+#endif
+__device__ __forceinline__ bool head_spilled(const uint4 &h, uint32_t gen) {
+    return RB_SPILL && h.y == gen && h.x > (uint32_t)BUCKET_SLOTS;
+}
+
 template <int RL = -1, typename T>
 __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, Claim c, const Snap<T> &sn,
                                              uint32_t tagged_id) {
@@ -238,7 +276,11 @@ __device__ __forceinline__ void publish_slot(const Table<T> &tab, int32_t *err, 
     // after the max the header carries gen (no later generation writes this
     // table before the next step's launch)
     const int32_t slot = (uint32_t)(c.old >> 32) == c.gen ? (int32_t)(uint32_t)c.old : BUCKET_SLOTS;
-    if (slot >= BUCKET_SLOTS) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
+    if (slot >= BUCKET_SLOTS) {
+        if ((uint32_t)(c.old >> 32) == c.gen) spill_insert(tab, err, c.b, tagged_id, c.gen);
+        else atomicOr(err, ERR_BUCKET_OVERFLOW);
+        return;
+    }
     wt_store(slot_word(tab, c.b, slot, RL >= 0 ? RL : c.rl), tagged_id);
     if (tab.pos) wt_store(tab.pos + (int64_t)c.b * LINE_WORDS + slot, sn);
 }
@@ -315,6 +357,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
     }
     STAMP(8);
     int32_t total = 0;
+    uint32_t spm = 0;                                 // buckets with spilled ids
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         int32_t n = head_count(hd[k], gen);
@@ -323,6 +366,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
             if (b[j] == b[k]) n = 0;                  // two cells hashed to one bucket: visit once
         c[k] = n;
         total += n;
+        if (n > 0 && head_spilled(hd[k], gen)) spm |= 1u << k;
     }
     int32_t np_ = 0;
     bool overflow = false;
@@ -368,6 +412,17 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
         base += RB_QBATCH;
         if (base == RB_QBATCH) STAMP(9);
     } while (base < total);
+    if (spm) {                                        // rare: ids past full buckets
+#pragma unroll 1
+        for (int k = 0; k < 8; ++k) {
+            if (!((spm >> k) & 1u)) continue;
+            spill_scan(p.cur, gen, b[k], [&](uint32_t t) {
+                const uint32_t j = t & ~BOX_FLAG;
+                if (j == (uint32_t)i) return;
+                if (hit(t, p.snap_cur[CHK(j, p.n_global)])) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)j, overflow);
+            });
+        }
+    }
     STAMP(10);
     if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
     return np_;
@@ -460,6 +515,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     STAMP(8);
     int32_t n = 0;
     bool more = false;
+    uint32_t spm = 0;                                 // buckets with spilled ids
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         int32_t m = head_count(hd[k].a, gen);
@@ -468,6 +524,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
             if (b[j] == b[k]) m = 0;                  // two cells hashed to one bucket: visit once
         c[k] = m;
         more |= m > WIDE_HEAD_IDS;
+        if (m > 0 && head_spilled(hd[k].a, gen)) spm |= 1u << k;
         // branch-free: every id is written at the list's end, which advances
         // only for a listed one (the last write lands at index <= WIDE_MAXC-1)
 #define RB_WIDE_LIST(S)                                                           \
@@ -540,6 +597,20 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                         else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
                     }
             }
+        }
+    }
+    if (RB_WIDE_MORE && spm) {                        // rarer: ids past full buckets (a spilled
+#pragma unroll 1                                      // bucket is a 7+ one: its index is stashed)
+        for (int k = 0; k < 8; ++k) {
+            if (!((spm >> k) & 1u)) continue;
+            spill_scan(p.cur, gen, s_cand[k * NB + tid], [&](uint32_t t) {
+                const uint32_t j = t & ~BOX_FLAG;
+                if (j == (uint32_t)i) return;
+                const Snap<T> sn = p.snap_cur[CHK(j, p.n_global)];
+                if (!hit(t, sn)) return;
+                if (RB_WIDE_LDSPOS) list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)j, sn, overflow);
+                else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)j, overflow);
+            });
         }
     }
     STAMP(10);

@@ -57,7 +57,13 @@ template <typename T> struct Table {
     uint32_t *line;            // [H / R][R x LINE_WORDS] bucket blocks: heads, then further ids
     Snap<T> *pos;              // [H][LINE_WORDS] slot snapshots (slot s at s); nullptr: not kept
     uint32_t *gen;             // this table's generation (device word)
+    uint32_t *spill;           // ids past a full bucket: header (generation << 32 | count), then
+                               // SPILL_CAP x {bucket, tagged id}; nullptr: none (an overflow is an error)
 };
+// A bucket holds 30 ids; a cell with more (a pile-up: C4's sliding rows
+// reach 29 by step 700) spills the rest into its table's spill list, which
+// a search reads only for a bucket whose count passed its slots.
+constexpr int SPILL_CAP = 8192;
 
 constexpr int MAX_PLANES = 8;
 

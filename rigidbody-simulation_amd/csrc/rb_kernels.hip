@@ -222,6 +222,14 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         for (int u = 0; u < QB; ++u)
             if (s0 + u < c && candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj[u], sn[u], defer)) mask |= 1u << (s0 + u);
     }
+    // rare: ids past a full bucket (rb_grid.hpp spill_scan), counted here,
+    // placed after the slot hits below (id-indexed snapshots: no slot copy)
+    int32_t hs = 0;
+    const bool spl = c > 0 && head_spilled(id4, gen);
+    if (spl)
+        spill_scan(p.cur, gen, b, [&](uint32_t t) {
+            if (candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, t, p.snap_cur[CHK(t & ~BOX_FLAG, p.n_global)], defer)) ++hs;
+        });
     STAMP(10);
     if (p.defer_q) {                              // any lane of the group: the body is deferred
         int dv = defer ? 1 : 0;
@@ -230,7 +238,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         dv |= __shfl_xor(dv, 4);
         defer = dv != 0;
     }
-    const int h = __popc(mask);
+    const int h = __popc(mask) + hs;
     int pre_n = 0, total = 0;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -257,6 +265,17 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
         }
         ++o;
     }
+    if (hs)
+        spill_scan(p.cur, gen, b, [&](uint32_t t) {
+            const Snap<T> sn = p.snap_cur[CHK(t & ~BOX_FLAG, p.n_global)];
+            bool d2 = false;
+            if (!candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, t, sn, d2)) return;
+            if (o < MAXP) {
+                t_id[slot * MAXP + o] = (int32_t)(t & ~BOX_FLAG);
+                t_pos[slot * MAXP + o] = sn;
+            }
+            ++o;
+        });
     __syncthreads();
     STAMP(11);
     const int tot = total < MAXP ? total : MAXP;
@@ -364,7 +383,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     }
     M3<T> M;                                       // box orientation (mj_kinematics of the free joint)
     if (kind != 0) M = mj_body_mat(q);
-    if (kind != 0) {
+    if (kind != 0 && !planes_done) {               // (a box's corners likewise)
         for (int pl = 0; pl < p.n_planes; ++pl) {
             const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
             const V3<T> dif = {x.x - p.pp[pl][0], x.y - p.pp[pl][1], x.z - p.pp[pl][2]};
@@ -668,14 +687,15 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
         bool planes = false;
         if (!p.xfrc) {
             apply_force(p, l, in.m, invI, in.v, in.w);
-            // a sphere's plane contacts come first in its contact order
-            // (body_update), so they are solved here too
+            // a body's plane contacts come first in its contact order
+            // (body_update: a sphere's one per plane, a box's corners), so
+            // they are solved here too
             const int32_t kind = ld.cs.kind[i];
+            const Snap<T> self = ld.snap_cur[i];
+            const V3<T> x = {self.x, self.y, self.z};
+            const T k = impulse_k(in.m);
             if (kind == 0) {
-                const Snap<T> self = ld.snap_cur[i];
-                const V3<T> x = {self.x, self.y, self.z};
                 const T rad = ld.cs.sx()[i];
-                const T k = impulse_k(in.m);
                 for (int pl = 0; pl < p.n_planes; ++pl) {
                     const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
                     const V3<T> pp = {p.pp[pl][0], p.pp[pl][1], p.pp[pl][2]};
@@ -684,8 +704,24 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
                     record(p, l, nrec, -1 - pl, 0, con.dist);
                     solve_contact(p, con, x, con.frame, in.m, k, invI, in.v, in.w);
                 }
-                planes = true;
+            } else {
+                const V3<T> sz = {ld.cs.sx()[i], ld.cs.sy()[i], ld.cs.sz()[i]};
+                const M3<T> M = mj_body_mat(in.q);
+                for (int pl = 0; pl < p.n_planes; ++pl) {
+                    const V3<T> pn = {p.pn[pl][0], p.pn[pl][1], p.pn[pl][2]};
+                    const V3<T> dif = {x.x - p.pp[pl][0], x.y - p.pp[pl][1], x.z - p.pp[pl][2]};
+                    const T dist = mj_dot(dif, pn);
+                    int cnt = 0;
+                    for (int c = 0; c < 8 && cnt < 4; ++c) {
+                        Contact<T> con;
+                        if (!plane_box_corner(pn, x, dist, M, sz, c, con)) continue;
+                        ++cnt;
+                        record(p, l, nrec, -1 - pl, 1 + c, con.dist);
+                        solve_contact(p, con, x, con.frame, in.m, k, invI, in.v, in.w);
+                    }
+                }
             }
+            planes = true;
         }
         T *o = s_help + h;
 #pragma unroll
@@ -993,7 +1029,7 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
         if (maxp <= 16) hipLaunchKernelGGL((search_kernel<T, 16, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         else hipLaunchKernelGGL((search_kernel<T, 32, GS>), dim3((unsigned)sblocks), dim3(STEP_BLOCK), 0, s, p);
         hipLaunchKernelGGL((update_kernel<T>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, p);
-    } else if (coop && form == FORM_COOP_HELP && !boxes) {
+    } else if (coop && form == FORM_COOP_HELP) {   // (box worlds: the box kernel follows)
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop_help<T, 16>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
         else hipLaunchKernelGGL((step_kernel_coop_help<T, 32>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     } else if (coop) {

@@ -81,7 +81,7 @@ SIGNATURES = {
 STAT_NAMES = ["graphs", "tile_runs", "tile_blocks", "tile_redo_taint", "tile_redo_bound", "tile_restart",
               "tile_fallback", "tile_steps", "form", "tiles", "tile_threads", "tile_kmax", "tile_cap",
               "tile_size_um", "tile_on", "box_opt_chunks", "box_rollbacks", "refits",
-              "table_grows", "buckets"]
+              "table_grows", "buckets", "max_partners"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
               3: "rb::step_kernel_coop_help"}
 

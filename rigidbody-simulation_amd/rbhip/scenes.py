@@ -255,6 +255,32 @@ def box_pile(nx: int, ny: int, layers: int = 3, seed: int = 0, spacing: float = 
                  _flat_plane(), np.array(qpos), qvel, dt=0.005, restitution=0.2, friction=0.6, threshold=0.0)
 
 
+def crowded_cells(nx: int = 10, ny: int = 10, layers: int = 4, seed: int = 0) -> Scene:
+    """Broadphase stress (no reference counterpart): one sphere of r 1.0 —
+    so cells are 4 m — far off, and nx*ny*layers spheres of r 0.05 (density
+    50) in a 0.12-m lattice dropped on flat ground: hundreds of bodies share
+    a cell, whose 128-B bucket holds 30 (the rest spill, rb_grid.hpp).
+    e 0.3, mu 0.4, dt 0.005."""
+    rng = np.random.default_rng(seed)
+    n = nx * ny * layers
+    m_s = 50.0 * 4.0 / 3.0 * np.pi * 0.05 ** 3
+    kind, mass, inertia, size = _spheres(n + 1, 0.05, m_s, 0.4 * m_s * 0.05 ** 2)
+    m_b = 50.0 * 4.0 / 3.0 * np.pi
+    mass[n], inertia[n], size[n] = m_b, 0.4 * m_b, [1.0, 0.0, 0.0]
+    iz, rem = np.divmod(np.arange(n), nx * ny)
+    iy, ix = np.divmod(rem, nx)
+    qpos = np.zeros((n + 1, 7))
+    qpos[:n, 0] = 0.3 + ix * 0.12 + rng.uniform(-0.005, 0.005, n)
+    qpos[:n, 1] = 0.3 + iy * 0.12 + rng.uniform(-0.005, 0.005, n)
+    qpos[:n, 2] = 0.06 + iz * 0.12 + rng.uniform(0.0, 0.01, n)
+    qpos[n, 0:3] = [12.0, 12.0, 1.0]
+    qpos[:, 3] = 1.0
+    qvel = np.zeros((n + 1, 6))
+    qvel[:n, 0:2] = rng.normal(0.0, 0.3, (n, 2))
+    return Scene(f"crowded_cells_{n + 1}", kind, mass, inertia, size, _flat_plane(), qpos, qvel,
+                 dt=0.005, restitution=0.3, friction=0.4, threshold=0.0)
+
+
 CONFIGS = {
     # BASELINE.json configs, in order
     "c1": single_sphere,

@@ -9,9 +9,8 @@
    65,536 bodies, with the positions moving between calls (fit_period's
    group-box cache) and with the same positions.
 2. Drift: the wall clock of step windows of one world, the
-   layout fitted once from the initial positions: C4 (201-350, 451-600:
-   later windows overflow a bucket, see drift()) and C3 translating across
-   its layout (261-460, 1,801-2,000).
+   layout fitted once from the initial positions: C4 and C3 translating
+   across its layout (261-460, 1,801-2,000).
 One JSON line per measurement.
 """
 from __future__ import annotations
@@ -83,13 +82,31 @@ def window_times(sc, windows, **kw):
 
 def drift():
     # C4: rows sliding down the incline pile into each other after ~550
-    # steps (up to 28 sphere partners; 29 bodies in one cell at step 700,
-    # one short of a bucket's 30: later steps overflow it) -> windows before
-    # that, max_partners 32
+    # steps (up to 28 sphere partners: max_partners 32; 29+ bodies per cell:
+    # full buckets spill); the layout stays the one fitted at t = 0
     sc = scenes.make("c4")
-    out = window_times(sc, [(201, 350), (451, 600)], max_partners=32)
-    print(json.dumps({"what": "C4: wall clock per step of step windows (one world, max_partners 32)", **out}),
-          flush=True)
+    out = window_times(sc, [(261, 460), (1801, 2000)], max_partners=32)
+    a, b = out["steps_261_460_us_per_step"], out["steps_1801_2000_us_per_step"]
+    print(json.dumps({"what": "C4: wall clock per step of step windows (one world, max_partners 32)", **out,
+                      "late_over_early": b / a}), flush=True)
+    # the same late window after a refit of the layout to the step-1,800
+    # positions (a get_state / set_state round trip refits at set_state)
+    with rbhip.World(sc, max_partners=32) as w:
+        w.step(1800)
+        q, v = w.get_state()
+        w.set_state(q, v)
+        w.step(200)                                  # graph capture (1,801-2,000)
+        q2, v2 = w.get_state()
+    with rbhip.World(sc, max_partners=32) as w:
+        w.set_state(q, v)
+        w.step(200)
+        w.set_state(q, v)
+        w.sync()
+        t, _ = timed(lambda: w.step(200))
+        q3, v3 = w.get_state()
+    assert np.array_equal(q2.view(np.uint64), q3.view(np.uint64))
+    print(json.dumps({"what": "C4 steps 1,801-2,000 with the layout refitted at step 1,800",
+                      "us_per_step": t / 200 * 1e6}), flush=True)
     # C3 translating at (10, 5) m/s: 200 m across its fitted layout by step 2,000
     sc = scenes.make("c3")
     qv = sc.qvel0.copy()

@@ -194,6 +194,57 @@ def test_bucket_overflow_rolls_back_and_refits_bit_exact(rb, oracle16, monkeypat
     assert st["table_grows"] == injected - 1 and st["buckets"] == h0 << (injected - 1), st
 
 
+@pytest.mark.parametrize("form,env", [("coop", {}), ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+                                      ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"})])
+def test_crowded_cells_spill_bit_exact(rb, oracle16, monkeypatch, form, env):
+    """Hundreds of bodies in one broadphase cell (scenes.crowded_cells: a
+    r 1.0 sphere sets 4-m cells, 400 spheres of r 0.05 pile up in one): the
+    ids past each bucket's 30 slots spill into the table's spill list, which
+    every search form reads for a full bucket — contacts (recorded steps) and
+    state bit-exact with the oracle, whose broadphase has no capacity."""
+    from rbhip import scenes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = scenes.crowded_cells()
+    cells = np.floor(sc.qpos0[:-1, :3] / (4.0 * 1.0 * 1.001)).astype(np.int64)
+    assert np.unique(cells, axis=0, return_counts=True)[1].max() > 30
+    osc = oracle16.OracleScene(sc)
+    q, v = sc.qpos0, sc.qvel0
+    with rb.World(sc) as w:
+        for t in (99, 99):
+            q, v = oracle16.step(osc, q, v, t)
+            w.step(t)
+            w.record_contacts(True)
+            q, v, (cnt, par, kin, dis) = oracle16.step(osc, q, v, 1, record=True)
+            w.step(1)
+            gc, gp, gk, gd = w.contacts()
+            w.record_contacts(False)
+            assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+            assert _same(gd, dis)
+            gq, gv = w.get_state()
+            assert _same(gq, q) and _same(gv, v)
+    assert cnt.sum() > 100                            # the pile is in contact
+
+
+@pytest.mark.timeout(900)
+def test_c4_2000_steps_bit_exact(rb, oracle16):
+    """configs[3]'s scene for 2,000 steps from t = 0 with the default world:
+    after ~550 steps the sliding rows pile into each other (up to 28 sphere
+    partners: a guarded rb_step chunk rolls back and raises max_partners to
+    32; up to 29+ bodies in a cell: full buckets spill) — bit-exact with the
+    oracle."""
+    from rbhip import scenes
+    sc = scenes.make("c4")
+    with rb.World(sc) as w:
+        for _ in range(4):
+            w.step(500)
+        q, v = w.get_state()
+        st = w.stats()
+    q1, v1 = oracle16.step(oracle16.OracleScene(sc, max_partners=32), sc.qpos0, sc.qvel0, 2000)
+    assert _same(q, q1) and _same(v, v1)
+    assert st["max_partners"] == 32, st
+
+
 def test_c3_one_step_parity_from_evolved_state(rb, oracle):
     """65,536 spheres: 30 oracle steps, then one GPU step from that state vs
     one oracle step (contacts and state bit-exact)."""
