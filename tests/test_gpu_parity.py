@@ -454,16 +454,36 @@ def test_nonfinite_position_is_an_error(rb):
             w.step(1)
 
 
-def test_box_pair_across_shards_is_unsupported(rb):
-    """Box-involved pairs are solved in unsharded worlds (tests/test_gpu_boxes.py);
-    a sharded world exchanges positions only, so one within contact range is
-    reported instead of being solved with a stale partner orientation."""
+def test_box_pair_across_shards_is_solved(rb):
+    """Two cubes within bounding range, one per shard: the exchange carries
+    their orientations (rb_gquat_buffer), so the pair is solved exactly as
+    in one world (this was RB_EUNSUPPORTED before round 3)."""
+    import torch
     from rbhip import scenes
+    from rbhip.shard import wrap_gpos, wrap_gquat
     sc = scenes.incline_cubes(2, 1, seed=0, spacing=0.5)
-    with rb.World(sc, rank=0, world_size=2) as w:
-        with pytest.raises(rb.RbError, match="EUNSUPPORTED"):
+    with rb.World(sc) as ref:
+        ref.step(60)
+        rq, rv = ref.get_state()
+    worlds = [rb.World(sc, rank=r, world_size=2) for r in range(2)]
+    for _ in range(60):
+        for w in worlds:
             w.shard_step()
+        for w in worlds:
             w.sync()
+        for wrap in (wrap_gpos, wrap_gquat):
+            (b0, n), (b1, _) = wrap(worlds[0], torch), wrap(worlds[1], torch)
+            b0[n:2 * n].copy_(b1[n:2 * n])
+            b1[0:n].copy_(b0[0:n])
+        torch.cuda.synchronize()
+        for w in worlds:
+            w.shard_exchange_done()
+    q = np.zeros((sc.n, 7))
+    v = np.zeros((sc.n, 6))
+    for w in worlds:
+        w.get_state(q, v)
+        w.close()
+    assert np.array_equal(q.view(np.uint64), rq.view(np.uint64)) and np.array_equal(v.view(np.uint64), rv.view(np.uint64))
 
 
 def test_kernel_timing_reports_launches(rb):
