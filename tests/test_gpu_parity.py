@@ -486,6 +486,23 @@ def test_box_pair_across_shards_is_solved(rb):
     assert np.array_equal(q.view(np.uint64), rq.view(np.uint64)) and np.array_equal(v.view(np.uint64), rv.view(np.uint64))
 
 
+def test_graph_cache_stays_bounded(rb):
+    """stepping with many different (K, dt, ...) keys keeps at
+    most GRAPH_CACHE_MAX (32) captured graphs alive (both parities of a key
+    are captured together; the least recently used are destroyed), and a
+    key evicted earlier is captured again when it comes back."""
+    from rbhip import scenes
+    with rb.World(scenes.flat_spheres(8, 8, seed=1)) as w:
+        seen = []
+        for k in range(40):
+            w.step(2 + k % 3, dt=0.01 + 1e-4 * k)
+            seen.append(w.stats()["graphs"])
+        w.step(2, dt=0.01)                        # the first key again
+        seen.append(w.stats()["graphs"])
+    assert max(seen) <= 32 and seen[-1] <= 32, seen
+    assert seen[0] == 2 and seen[15] == 32, seen  # two entries per key until the cap
+
+
 def test_kernel_timing_reports_launches(rb):
     from rbhip import scenes
     with rb.World(scenes.make("c2")) as w:
