@@ -685,7 +685,7 @@ size_t chunk_save_bytes(const rb_world *w) {
 int chunk_save(rb_world *w) {
     if (!w->opt_save) {
         HIPCHK(hipMalloc(&w->opt_save, chunk_save_bytes(w)));
-        HIPCHK(hipHostMalloc((void **)&w->defer_host, sizeof(int32_t) * 3, 0));
+        HIPCHK(hipHostMalloc((void **)&w->defer_host, sizeof(int32_t) * 4, 0));
     }
     char *o = static_cast<char *>(w->opt_save);
     const size_t st = (size_t)w->esz * 13 * w->S, sn = (size_t)w->esz * 4 * w->Npad;
@@ -693,6 +693,8 @@ int chunk_save(rb_world *w) {
     HIPCHK(hipMemcpyAsync(o + st, w->snap[w->sp()], sn, hipMemcpyDeviceToDevice, w->stream));
     if (w->boxes) HIPCHK(hipMemcpyAsync(o + st + sn, w->qsnap[w->sp()], sn, hipMemcpyDeviceToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(o + st + 2 * sn, w->err, sizeof(int32_t), hipMemcpyDeviceToDevice, w->stream));
+    // the error bits from before the chunk (an earlier rb_step_async), read with the check
+    HIPCHK(hipMemcpyAsync(w->defer_host + 3, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
     if (w->boxes) HIPCHK(hipMemsetAsync(w->defer_cnt, 0, sizeof(int32_t) * 2, w->stream));
     return RB_OK;
 }
@@ -700,7 +702,7 @@ int chunk_check(rb_world *w, int32_t &err, bool &deferred) {
     HIPCHK(hipMemcpyAsync(w->defer_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
     if (w->boxes) HIPCHK(hipMemcpyAsync(w->defer_host + 1, w->defer_cnt, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
-    err = w->defer_host[0];
+    err = w->defer_host[0] & ~w->defer_host[3];       // raised during this chunk
     if (w->diag_overflow > 0) { --w->diag_overflow; err |= ERR_BUCKET_OVERFLOW; }
     deferred = w->boxes && (w->defer_host[1] | w->defer_host[2]) != 0;
     return RB_OK;
