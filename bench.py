@@ -47,7 +47,9 @@ step-kernel launches, / K.  Several ranks: an event pair around each
 step-kernel launch over a second run of K steps.  `traffic` /
 `traffic_lower`: the PMC bounds per launch from the committed
 profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
-command, profiles/collect_pmc.py), named in `traffic_source`.
+command, profiles/collect_pmc.py), named in `traffic_source`;
+`traffic_same_build` says whether they were collected on the library build
+this run loaded (the file records its hash).
 cpu_baseline (rank 0, N = 1): the oracle (C restatement of the reference
 arithmetic) over the full single-GPU scene for --cpu-steps steps from t = 0,
 on the host-core share (OMP_NUM_THREADS if set, else the affinity mask) and
@@ -286,8 +288,15 @@ def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str):
     except (OSError, ValueError):
         e = None
     if not e:
-        return None, None, None
-    return e.get("hbm_bytes_per_launch"), e.get("hbm_bytes_per_launch_lower"), f"{rel}[{key}]"
+        return None, None, None, None
+    import hashlib
+    lib = os.path.join(ROOT, "rigidbody-simulation_amd", "rbhip", "librbhip.so")
+    try:
+        with open(lib, "rb") as f:
+            same = hashlib.sha256(f.read()).hexdigest()[:16] == e.get("librbhip_sha16")
+    except OSError:
+        same = False
+    return e.get("hbm_bytes_per_launch"), e.get("hbm_bytes_per_launch_lower"), f"{rel}[{key}]", same
 
 
 def main():
@@ -410,7 +419,8 @@ def main():
         timing = "HIP event pair around each step-kernel launch (second run of K steps)"
     bytes_per_launch = w.bytes_per_body_step * w.n_owned
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, traffic_lower, traffic_src = traffic_from_profiles(args.config, args.dtype, P, args.scaling)
+    traffic, traffic_lower, traffic_src, traffic_same_build = traffic_from_profiles(args.config, args.dtype, P,
+                                                                                    args.scaling)
 
     value = scene.n * args.steps / elapsed
     line = {
@@ -438,6 +448,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": traffic_lower,
                      "traffic_source": traffic_src,
+                     # the counters were collected on this very library build
+                     "traffic_same_build": traffic_same_build,
                      "kernel": step_kernel_name(st1, tiled),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,

@@ -64,7 +64,12 @@ def main():
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
     key = f"{cfg}_{dtype}" if P == 1 else f"{cfg}_{dtype}_p{P}"
+    import hashlib
+    lib = os.path.join(ROOT, "rigidbody-simulation_amd", "rbhip", "librbhip.so")
     data[key] = {
+        # the library build the counters saw (bench.py flags a line whose
+        # library differs: the figures may then be stale)
+        "librbhip_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
         "fetch_size_kb_per_launch": f, "write_size_kb_per_launch": w,
         "hbm_bytes_per_launch": guide,
         "hbm_bytes_per_launch_lower": f * 1024.0 + w * 1024.0,
