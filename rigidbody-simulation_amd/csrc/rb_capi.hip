@@ -1421,6 +1421,10 @@ static int fit_tiles(rb_world *w, const double *qpos) {
     // auto mode allocates the bins only for scenes it would tile
     if (w->tile_mode < 0 && w->N < w->tile_min_bodies) { w->tile_ntx = 0; return RB_OK; }
     w->tile_nt = w->dtype == RB_F64 ? 512 : 768;
+    // RBHIP_TILE_NT=256 (fp64): small tiles, one wave per SIMD across the
+    // chip for small scenes (a strong-scaling shard)
+    if (const char *ev = getenv("RBHIP_TILE_NT"))
+        if (w->dtype == RB_F64 && atoi(ev) == 256) w->tile_nt = 256;
     double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
     int64_t nf = 0;
     for (int64_t b = 0; b < w->N; ++b) {

@@ -864,8 +864,9 @@ template <typename T> hipError_t launch_tile_gather(const TileParams<T> &p, hipS
 template <typename T> hipError_t launch_tile_block(const TileParams<T> &p, int nt, hipStream_t s) {
     // fp64: 512 threads (206 VGPRs, 2 waves per SIMD, no spill); fp32: 768
     if constexpr (sizeof(T) == 8) {
-        if (nt != 512) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((tile_block_kernel<T, 512>), dim3((unsigned)p.ntile), dim3(512), 0, s, p);
+        if (nt == 256) hipLaunchKernelGGL((tile_block_kernel<T, 256>), dim3((unsigned)p.ntile), dim3(256), 0, s, p);
+        else if (nt == 512) hipLaunchKernelGGL((tile_block_kernel<T, 512>), dim3((unsigned)p.ntile), dim3(512), 0, s, p);
+        else return hipErrorInvalidValue;
     } else {
         if (nt != 768) return hipErrorInvalidValue;
         hipLaunchKernelGGL((tile_block_kernel<T, 768>), dim3((unsigned)p.ntile), dim3(768), 0, s, p);

@@ -503,6 +503,47 @@ def test_graph_cache_stays_bounded(rb):
     assert seen[0] == 2 and seen[15] == 32, seen  # two entries per key until the cap
 
 
+def test_empty_world_and_idle_shards(rb):
+    """Edge cases: a world with no bodies is refused (RB_EINVAL, "n_bodies
+    out of range": nothing to step, and no device buffers of size 0); a
+    3-body scene over 4 shards (rank 3 owns no body) matches one world."""
+    import torch
+    from rbhip import scenes
+    from rbhip.shard import wrap_gpos
+    sc0 = scenes.flat_spheres(2, 2).with_(kind=np.zeros(0, np.int32), mass=np.zeros(0), inertia=np.zeros((0, 3)),
+                                         size=np.zeros((0, 3)), qpos0=np.zeros((0, 7)), qvel0=np.zeros((0, 6)))
+    with pytest.raises(rb.RbError, match="EINVAL"):
+        rb.World(sc0)
+    sc = scenes.multi_sphere4().with_()
+    sc = sc.with_(kind=sc.kind[:3], mass=sc.mass[:3], inertia=sc.inertia[:3], size=sc.size[:3],
+                  qpos0=sc.qpos0[:3], qvel0=sc.qvel0[:3], names=None)
+    with rb.World(sc) as ref:
+        ref.step(200)
+        rq, rv = ref.get_state()
+    worlds = [rb.World(sc, rank=r, world_size=4) for r in range(4)]
+    assert [w.n_owned for w in worlds] == [1, 1, 1, 0]
+    for _ in range(200):
+        for w in worlds:
+            w.shard_step()
+        for w in worlds:
+            w.sync()
+        bufs = [wrap_gpos(w, torch) for w in worlds]
+        n = bufs[0][1]
+        for r, (buf, _) in enumerate(bufs):
+            for o, (obuf, _) in enumerate(bufs):
+                if o != r:
+                    buf[o * n:(o + 1) * n].copy_(obuf[o * n:(o + 1) * n])
+        torch.cuda.synchronize()
+        for w in worlds:
+            w.shard_exchange_done()
+    q = np.zeros((3, 7))
+    v = np.zeros((3, 6))
+    for w in worlds:
+        w.get_state(q, v)
+        w.close()
+    assert np.array_equal(q.view(np.uint64), rq.view(np.uint64)) and np.array_equal(v.view(np.uint64), rv.view(np.uint64))
+
+
 def test_kernel_timing_reports_launches(rb):
     from rbhip import scenes
     with rb.World(scenes.make("c2")) as w:
