@@ -337,8 +337,9 @@ def main():
 
     # N > 1: both peer-to-peer modes (halo pushes, full slice reads) are
     # warmed up, validated against one World and timed over PROBE steps on
-    # this node's xGMI; the faster valid one runs the timed region.  RCCL is
-    # the fallback when neither validates.
+    # this node's xGMI; the faster valid one runs the timed region.  The
+    # in-library RCCL exchange is the fallback when neither validates, and
+    # torch.distributed's all-gather (host-driven) the last one.
     PROBE = 20
     done = args.warmup
     if P == 1:
@@ -347,8 +348,9 @@ def main():
         probes = {}
     else:
         cands, probes = [], {}
-        for tr, halo in (("p2p", True), ("p2p", False), ("rccl", "auto")):
-            if tr == "rccl" and cands:
+        # last resort: torch.distributed's all-gather per step (host-driven)
+        for tr, halo in (("p2p", True), ("p2p", False), ("rccl", "auto"), ("nccl", False)):
+            if tr in ("rccl", "nccl") and cands:
                 break
             c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo)
             name = c.transport + (" halo" if c.halo else " full reads" if c.transport == "p2p" else "")
