@@ -1108,6 +1108,11 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // records per body: 4 per plane, 1 per sphere partner, up to 4 per
     // partner in scenes with boxes (oracle/rb_oracle_impl.h contact_stride)
     w->maxrec = 4 * w->n_planes + (any_box ? 4 : 1) * w->maxp;
+    // worlds with boxes: the cooperative form only up to 4,608 owned bodies
+    // (cubes on the incline, per step, helper / plain cooperative / wide:
+    // 4,096 8.6 / 10.7 / 11.7 us, 5,184 10.4 / 12.4 / 10.2, 9,216 12.9 /
+    // 15.7 / 10.2, 16,384 14.7 (plain) / 12.2; scripts/form_ab.py)
+    if (any_box) w->coop_max = 4608;
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
