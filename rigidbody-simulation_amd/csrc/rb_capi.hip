@@ -89,6 +89,10 @@ struct rb_world {
     // lanes' chain): 4k 8.1 -> 7.4 us, 8k 9.6 -> 8.6; 16k 11.0 -> 11.9 the
     // other way (its waves then share SIMDs)
     int64_t help_max = 12288;
+    // the wide form with a helper wave per workgroup (inv(I_w), gravity,
+    // plane contacts and the v / w / I loads off the body wave): 25.6k 13.4
+    // -> 12.8 us, 32k 13.6 -> 13.0, 65k 16.9 -> 16.4, C4 15.4 -> 14.9
+    bool wide_help = true;
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};
     double inv_cs = 1.0;
@@ -318,7 +322,7 @@ int prime(rb_world *w, double dt = 0, double e = 0, double mu = 0) {
 // the per-step kernel form of this world
 int step_form(const rb_world *w) {
     return w->n_local <= w->coop_max ? (w->n_local <= w->help_max ? FORM_COOP_HELP : FORM_COOP)
-           : w->n_local <= w->wide_max ? FORM_WIDE : FORM_ONE;
+           : w->n_local <= w->wide_max ? (w->wide_help ? FORM_WIDE_HELP : FORM_WIDE) : FORM_ONE;
 }
 
 int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, double mu, double thr) {
@@ -1116,6 +1120,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_COOP_MAX_BODIES")) w->coop_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
+    if (const char *ev = getenv("RBHIP_WIDE_HELP")) w->wide_help = atoi(ev) != 0;
     // K-step tile blocks (rb_tile.hip): RBHIP_TILE = 0 off, 1 on, unset auto
     // (sphere worlds of >= RBHIP_TILE_MIN_BODIES on one rank)
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) ? 1 : 0;

@@ -331,11 +331,11 @@ template <typename T> hipError_t launch_tile_scatter(const TileParams<T> &p, hip
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one
 // lane per body at one wave per SIMD (mid-size scenes)
-enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3 };
+enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4 };
 // boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
 // the wide form's kernel alone (its own translation unit: scheduled for memory clauses)
-template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, hipStream_t s);
+template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, bool help, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip

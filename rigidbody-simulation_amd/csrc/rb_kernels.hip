@@ -305,8 +305,12 @@ __device__ __forceinline__ BodyIn<T> load_body(const BodyState<T> &st, const Bod
     b.q = {st.qw()[l], st.qx()[l], st.qy()[l], st.qz()[l]};
     b.v = {st.vx()[l], st.vy()[l], st.vz()[l]};
     b.w = {st.wx()[l], st.wy()[l], st.wz()[l]};
-    b.m = cs.mass()[i];
-    b.I = {cs.ix()[i], cs.iy()[i], cs.iz()[i]};
+    // diagnostic (RB_ABLATE 8): every body reads body 0's constants (a
+    // scene of identical bodies stays bit-exact) — the cost of the per-body
+    // constant loads
+    const int32_t ci = RB_ABLATE == 8 ? 0 : i;
+    b.m = cs.mass()[ci];
+    b.I = {cs.ix()[ci], cs.iy()[ci], cs.iz()[ci]};
     return b;
 }
 template <typename T> __device__ __forceinline__ BodyIn<T> load_body(const StepParams<T> &p, int32_t l, int32_t i) {
@@ -538,19 +542,25 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
     // ---- K1 first: the contact search reads only step-start data -----------
     const Snap<T> self = ld.snap_cur[i];
     const V3<T> x = {self.x, self.y, self.z};
-    const int32_t kind = ld.cs.kind[i];
+    const int32_t ci = RB_ABLATE == 8 ? 0 : i;    // (diagnostic, load_body)
+    const int32_t kind = ld.cs.kind[ci];
     const T bi = self.r;
     // half extents y, z only matter for boxes; loaded for every body (a load
     // under a kind test would wait for kind before the state loads issue)
-    const T sy = ld.cs.sy()[i], szz = ld.cs.sz()[i];
-    const V3<T> sz = {ld.cs.sx()[i], kind != 0 ? sy : T(0), kind != 0 ? szz : T(0)};
+    const T sy = ld.cs.sy()[ci], szz = ld.cs.sz()[ci];
+    const V3<T> sz = {ld.cs.sx()[ci], kind != 0 ? sy : T(0), kind != 0 ? szz : T(0)};
     BodyIn<T> in;
     LazyInvI<T> invI;
     bool forced = false;
     // state loads issued before the search (the wide form measured 5 % slower
     // with them issued after the bucket heads, C3)
     constexpr bool early = G > 1 || WIDE;
-    if constexpr (early) {
+    if constexpr (early && HELP) {
+        // the helper wave loads v, w and I (help_body) and hands over inv(I_w)
+        // and the post-gravity, post-plane v and w: only q and m here
+        in.q = {ld.st.qw()[l], ld.st.qx()[l], ld.st.qy()[l], ld.st.qz()[l]};
+        in.m = ld.cs.mass()[RB_ABLATE == 8 ? 0 : i];
+    } else if constexpr (early) {
         in = load_body(ld.st, ld.cs, l, i);
         invI.I = in.I;
         invI.q = in.q;
@@ -567,7 +577,16 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
     STAMP(1);
     int32_t np_ = 0;
     bool defer = false;                          // a box-involved partner in range: the box kernel steps it
-    if constexpr (G == 1 && WIDE) {
+    if constexpr (G == 1 && WIDE && HELP) {
+        // the helper wave evaluates inv(I_w), gravity and the plane contacts
+        // (help_body); every lane of the body wave takes part in its two
+        // barriers, so the search runs under the active mask only
+        if (RB_ABLATE != 1 && active)
+            np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, s_didx, s_hpos, tid, gen,
+                                                       defer, [] {});
+        __syncthreads();                         // the search is done with s_cand: the helper fills it
+        __syncthreads();
+    } else if constexpr (G == 1 && WIDE) {
         if (RB_ABLATE != 1)
             np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, s_didx, s_hpos, tid, gen,
                                                        defer, [&] {
@@ -623,6 +642,9 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
             in.v = {o[9 * NBH], o[10 * NBH], o[11 * NBH]};
             in.w = {o[12 * NBH], o[13 * NBH], o[14 * NBH]};
             forced = true;
+        } else {                                 // applied forces: the body lanes apply them
+            in.v = {p.st.vx()[l], p.st.vy()[l], p.st.vz()[l]};
+            in.w = {p.st.wx()[l], p.st.wy()[l], p.st.wz()[l]};
         }
         const T pr = o[15 * NBH];
         help_planes = pr >= T(0);
@@ -672,7 +694,11 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
 // recorded-contact count in LDS (column layout, 16 reals per body) before
 // the search's first barrier; it then takes part in the search's two
 // barriers.  The same arithmetic in the same order, so bit-identical.
-template <typename T, int NB>
+//
+// WIDE (step_kernel_wide_help): the results go to the body wave's candidate
+// list area once its search is done with it (between the two barriers),
+// so the workgroup's LDS stays within a quarter of the CU's.
+template <typename T, int NB, bool WIDE = false>
 __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> &ld, int h, T *s_help) {
     // the same block -> bodies mapping as the body lanes (step_body)
     const int64_t hb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + h;
@@ -723,14 +749,18 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
             }
             planes = true;
         }
+        if (WIDE) __syncthreads();               // the body wave's search is done with s_cand
         T *o = s_help + h;
 #pragma unroll
         for (int e = 0; e < 9; ++e) o[e * NB] = m.a[e];
         o[9 * NB] = in.v.x; o[10 * NB] = in.v.y; o[11 * NB] = in.v.z;
         o[12 * NB] = in.w.x; o[13 * NB] = in.w.y; o[14 * NB] = in.w.z;
         o[15 * NB] = T(planes ? nrec : -1);
+        __syncthreads();
+        if (!WIDE) __syncthreads();              // search_coop's two barriers
+        return;
     }
-    __syncthreads();                             // search_coop's two barriers
+    __syncthreads();
     __syncthreads();
 }
 
@@ -745,13 +775,16 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
-    __shared__ T s_help[HELP ? 16 * NB : 1];
+    // the wide form's helper results share the candidate list's area
+    __shared__ T s_help[HELP && !WIDE ? 16 * NB : 1];
+    static_assert(!WIDE || sizeof(uint32_t) * WIDE_MAXC >= 16 * sizeof(T), "helper results fit in s_cand");
+    T *const help_lds = WIDE ? reinterpret_cast<T *>(s_cand) : s_help;
     const int tid = threadIdx.x;
     if (RB_ABLATE == 3) return;
     if constexpr (HELP) {
-        static_assert(G > 1 && !WIDE && !BOXES, "helper waves: the cooperative sphere form");
+        static_assert(!BOXES, "helper waves: the sphere step kernels");
         if (tid >= STEP_BLOCK) {                 // the workgroup's second wave
-            help_body<T, NB>(p, ld, tid - STEP_BLOCK, s_help);
+            help_body<T, NB, WIDE>(p, ld, tid - STEP_BLOCK, help_lds);
             return;
         }
     }
@@ -774,9 +807,9 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
     const bool active = lb < ld.n_local;
     int32_t cell[3] = {INT32_MAX, 0, 0};
-    if (G > 1 || active)
+    if (G > 1 || HELP || active)                 // (a helper's barriers: every lane)
         body_step<T, MAXP, G, WIDE, BOXES, true, HELP>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand,
-                                                       cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, s_help);
+                                                       cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, help_lds);
     if (p.bounds) fold_bounds(p.bounds, cell);
     if (blockIdx.x == 0 && tid == 0) {
         if (p.next.line) *p.next.gen = *p.cur.gen + 1u;
@@ -858,6 +891,16 @@ __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1
 void step_kernel_wide(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
                       const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
     step_body<T, MAXP, 1, true, false>(
+        p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
+}
+
+// the wide form with a helper wave per workgroup (help_body): two waves per
+// SIMD, each within 256 registers
+template <typename T, int MAXP>
+__global__ __launch_bounds__(2 * STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void step_kernel_wide_help(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
+                           const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
+    step_body<T, MAXP, 1, true, false, true>(
         p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
 }
 
@@ -1035,8 +1078,8 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
     } else if (coop) {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_coop<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
         else hipLaunchKernelGGL((step_kernel_coop<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
-    } else if (form == FORM_WIDE) {
-        const hipError_t we = launch_step_wide<T>(p, maxp, s);
+    } else if (form == FORM_WIDE || form == FORM_WIDE_HELP) {
+        const hipError_t we = launch_step_wide<T>(p, maxp, form == FORM_WIDE_HELP, s);
         if (we != hipSuccess) return we;
     } else {
         if (maxp <= 16) hipLaunchKernelGGL((step_kernel_one<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
@@ -1082,9 +1125,14 @@ template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, 
     return hipGetLastError();
 }
 
-template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, hipStream_t s) {
+template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, bool help, hipStream_t s) {
     int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
     if (blocks < 1) blocks = 1;
+    if (help) {
+        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide_help<T, 16>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+        else hipLaunchKernelGGL((step_kernel_wide_help<T, 32>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+        return hipGetLastError();
+    }
     if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
     return hipGetLastError();
@@ -1101,10 +1149,10 @@ template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int ma
 #define RB_WIDE_UNIT 2                  // both (a one-command build of all sources)
 #endif
 #if RB_WIDE_UNIT >= 1 && (RB_INST & 1)
-template hipError_t launch_step_wide<double>(const StepParams<double> &, int, hipStream_t);
+template hipError_t launch_step_wide<double>(const StepParams<double> &, int, bool, hipStream_t);
 #endif
 #if RB_WIDE_UNIT >= 1 && (RB_INST & 2)
-template hipError_t launch_step_wide<float>(const StepParams<float> &, int, hipStream_t);
+template hipError_t launch_step_wide<float>(const StepParams<float> &, int, bool, hipStream_t);
 #endif
 #if RB_WIDE_UNIT != 1 && (RB_INST & 1)
 template hipError_t launch_step<double>(const StepParams<double> &, int, int, bool, hipStream_t);
