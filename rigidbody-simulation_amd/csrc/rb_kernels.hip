@@ -556,10 +556,9 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
     // with them issued after the bucket heads, C3)
     constexpr bool early = G > 1 || WIDE;
     if constexpr (early && HELP) {
-        // the helper wave loads v, w and I (help_body) and hands over inv(I_w)
-        // and the post-gravity, post-plane v and w: only q and m here
-        in.q = {ld.st.qw()[l], ld.st.qx()[l], ld.st.qy()[l], ld.st.qz()[l]};
-        in.m = ld.cs.mass()[RB_ABLATE == 8 ? 0 : i];
+        // the helper wave loads the state and constants (help_body) and hands
+        // over q, m, inv(I_w) and the post-gravity, post-plane v and w: the
+        // body lanes load only what the search needs
     } else if constexpr (early) {
         in = load_body(ld.st, ld.cs, l, i);
         invI.I = in.I;
@@ -646,6 +645,8 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
             in.v = {p.st.vx()[l], p.st.vy()[l], p.st.vz()[l]};
             in.w = {p.st.wx()[l], p.st.wy()[l], p.st.wz()[l]};
         }
+        in.q = {o[16 * NBH], o[17 * NBH], o[18 * NBH], o[19 * NBH]};
+        in.m = o[20 * NBH];
         const T pr = o[15 * NBH];
         help_planes = pr >= T(0);
         help_nrec = help_planes ? (int32_t)pr : 0;
@@ -691,26 +692,33 @@ __device__ __forceinline__ void fold_bounds(int32_t *bounds, const int32_t *cell
 // workgroup evaluates inv(I_w), gravity and a sphere's plane contacts (the
 // first in its contact order) — VALU chain the body lanes otherwise run
 // under or after their bucket loads — and leaves inv(I_w), v, w and the
-// recorded-contact count in LDS (column layout, 16 reals per body) before
+// recorded-contact count, q and m in LDS (column layout, HELP_REALS per body) before
 // the search's first barrier; it then takes part in the search's two
 // barriers.  The same arithmetic in the same order, so bit-identical.
 //
 // WIDE (step_kernel_wide_help): the results go to the body wave's candidate
 // list area once its search is done with it (between the two barriers),
 // so the workgroup's LDS stays within a quarter of the CU's.
+constexpr int HELP_REALS = 21;                   // inv(I_w) 9, v 3, w 3, records 1, q 4, m 1
 template <typename T, int NB, bool WIDE = false>
 __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> &ld, int h, T *s_help) {
     // the same block -> bodies mapping as the body lanes (step_body)
     const int64_t hb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + h;
-    if (h < NB && hb < ld.n_local) {
+    const bool act = h < NB && hb < ld.n_local;
+    // results kept in registers across the wide form's first barrier; the
+    // barriers themselves are outside every divergent branch (a barrier in
+    // a branch taken by some lanes of the wave would be issued once per path)
+    BodyIn<T> in{};
+    M3<T> m{};
+    int32_t nrec = 0;
+    bool planes = false;
+    if (act) {
         const int32_t l = (int32_t)hb, i = ld.lo + l;
-        BodyIn<T> in = load_body(ld.st, ld.cs, l, i);
+        in = load_body(ld.st, ld.cs, l, i);
         LazyInvI<T> invI;
         invI.I = in.I;
         invI.q = in.q;
-        const M3<T> m = invI.get();
-        int32_t nrec = 0;
-        bool planes = false;
+        m = invI.get();
         if (!p.xfrc) {
             apply_force(p, l, in.m, invI, in.v, in.w);
             // a body's plane contacts come first in its contact order
@@ -749,19 +757,20 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
             }
             planes = true;
         }
-        if (WIDE) __syncthreads();               // the body wave's search is done with s_cand
+    }
+    if (WIDE) __syncthreads();                   // the body wave's search is done with s_cand
+    if (act) {
         T *o = s_help + h;
 #pragma unroll
         for (int e = 0; e < 9; ++e) o[e * NB] = m.a[e];
         o[9 * NB] = in.v.x; o[10 * NB] = in.v.y; o[11 * NB] = in.v.z;
         o[12 * NB] = in.w.x; o[13 * NB] = in.w.y; o[14 * NB] = in.w.z;
         o[15 * NB] = T(planes ? nrec : -1);
-        __syncthreads();
-        if (!WIDE) __syncthreads();              // search_coop's two barriers
-        return;
+        o[16 * NB] = in.q.w; o[17 * NB] = in.q.x; o[18 * NB] = in.q.y; o[19 * NB] = in.q.z;
+        o[20 * NB] = in.m;
     }
     __syncthreads();
-    __syncthreads();
+    if (!WIDE) __syncthreads();                  // search_coop's two barriers
 }
 
 template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false, bool HELP = false>
@@ -776,8 +785,8 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> t_pos[G > 1 ? MAXP * NB : 1];
     // the wide form's helper results share the candidate list's area
-    __shared__ T s_help[HELP && !WIDE ? 16 * NB : 1];
-    static_assert(!WIDE || sizeof(uint32_t) * WIDE_MAXC >= 16 * sizeof(T), "helper results fit in s_cand");
+    __shared__ T s_help[HELP && !WIDE ? HELP_REALS * NB : 1];
+    static_assert(!WIDE || sizeof(uint32_t) * WIDE_MAXC >= HELP_REALS * sizeof(T), "helper results fit in s_cand");
     T *const help_lds = WIDE ? reinterpret_cast<T *>(s_cand) : s_help;
     const int tid = threadIdx.x;
     if (RB_ABLATE == 3) return;

@@ -58,6 +58,7 @@ def test_kat_narrow_f32_matches_f32_restatement(rb, oracle):
 
 
 @pytest.mark.parametrize("form,env", [("coop", {}), ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+                                      ("wide_plain", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_HELP": "0"}),
                                       ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"})])
 def test_box_pile_bit_exact(rb, oracle, monkeypatch, form, env):
     """Tilted cube columns with sphere caps (rbhip.scenes.box_pile) landing,
@@ -129,6 +130,7 @@ def _approaching_boxes():
 
 
 @pytest.mark.parametrize("form,env", [("coop", {}), ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+                                      ("wide_plain", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_HELP": "0"}),
                                       ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"})])
 def test_boxes_entering_range_bit_exact(rb, oracle, monkeypatch, form, env):
     """Boxes stepped by the sphere kernel (no box partner in range) must

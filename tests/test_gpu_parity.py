@@ -195,6 +195,7 @@ def test_bucket_overflow_rolls_back_and_refits_bit_exact(rb, oracle16, monkeypat
 
 
 @pytest.mark.parametrize("form,env", [("coop", {}), ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+                                      ("wide_plain", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_HELP": "0"}),
                                       ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"})])
 def test_crowded_cells_spill_bit_exact(rb, oracle16, monkeypatch, form, env):
     """Hundreds of bodies in one broadphase cell (scenes.crowded_cells: a
@@ -339,8 +340,14 @@ def test_f32_vs_f64_tolerance_sweep(rb, oracle, horizon, max_flip_frac, med_rel,
         assert d.max() < max_d
 
 
-def test_xfrc_applied_matches_oracle(rb, oracle):
+@pytest.mark.parametrize("env", [{}, {"RBHIP_COOP_MAX_BODIES": "0"}, {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_HELP": "0"}],
+                         ids=["coop_help", "wide_help", "wide_plain"])
+def test_xfrc_applied_matches_oracle(rb, oracle, monkeypatch, env):
+    """Applied forces (collision.py:66-70): the helper-wave forms leave them
+    to the body lanes."""
     from rbhip import scenes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     sc = scenes.flat_spheres(16, 16, seed=5)
     rng = np.random.default_rng(0)
     xf = rng.normal(0, 0.5, (sc.n, 6))
@@ -603,6 +610,7 @@ def test_wide_form_buckets_past_the_head_bit_exact(rb, oracle, monkeypatch):
     ("coop", {}),
     ("coop_help", {"RBHIP_HELP_MAX_BODIES": "100000"}),
     ("wide", {"RBHIP_COOP_MAX_BODIES": "0"}),
+    ("wide_plain", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_HELP": "0"}),
     ("one", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0"}),
     ("split", {"RBHIP_COOP_MAX_BODIES": "0", "RBHIP_WIDE_MAX_BODIES": "0", "RBHIP_SPLIT": "1"}),
 ])
