@@ -90,8 +90,9 @@ struct rb_world {
     // other way (its waves then share SIMDs)
     int64_t help_max = 12288;
     // the wide form with a helper wave per workgroup (inv(I_w), gravity,
-    // plane contacts and the v / w / I loads off the body wave): 25.6k 13.4
-    // -> 12.8 us, 32k 13.6 -> 13.0, 65k 16.9 -> 16.4, C4 15.4 -> 14.9
+    // plane contacts and the state / constant loads off the body wave;
+    // A/B steps 261-460, profiles/r03/wide_help_ab.txt): 32k 13.6 -> 12.9
+    // us, C3 16.8 -> 16.1, C4 15.4 -> 14.9, C5 (16,384 cubes) 12.1 -> 9.6
     bool wide_help = true;
     double planes[RB_MAX_PLANES][6] = {};
     double g[3] = {};

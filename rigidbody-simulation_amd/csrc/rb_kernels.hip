@@ -555,10 +555,12 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
     // state loads issued before the search (the wide form measured 5 % slower
     // with them issued after the bucket heads, C3)
     constexpr bool early = G > 1 || WIDE;
-    if constexpr (early && HELP) {
+    if constexpr (early && HELP && WIDE) {
         // the helper wave loads the state and constants (help_body) and hands
         // over q, m, inv(I_w) and the post-gravity, post-plane v and w: the
-        // body lanes load only what the search needs
+        // body lanes load only what the search needs (the cooperative form
+        // keeps its own loads: handing q, m over there measured 4,096 bodies
+        // 7.4 -> 7.9 us, 8,190 8.6 -> 9.0)
     } else if constexpr (early) {
         in = load_body(ld.st, ld.cs, l, i);
         invI.I = in.I;
@@ -641,12 +643,14 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
             in.v = {o[9 * NBH], o[10 * NBH], o[11 * NBH]};
             in.w = {o[12 * NBH], o[13 * NBH], o[14 * NBH]};
             forced = true;
-        } else {                                 // applied forces: the body lanes apply them
+        } else if constexpr (WIDE) {             // applied forces: the body lanes apply them
             in.v = {p.st.vx()[l], p.st.vy()[l], p.st.vz()[l]};
             in.w = {p.st.wx()[l], p.st.wy()[l], p.st.wz()[l]};
         }
-        in.q = {o[16 * NBH], o[17 * NBH], o[18 * NBH], o[19 * NBH]};
-        in.m = o[20 * NBH];
+        if constexpr (WIDE) {
+            in.q = {o[16 * NBH], o[17 * NBH], o[18 * NBH], o[19 * NBH]};
+            in.m = o[20 * NBH];
+        }
         const T pr = o[15 * NBH];
         help_planes = pr >= T(0);
         help_nrec = help_planes ? (int32_t)pr : 0;
