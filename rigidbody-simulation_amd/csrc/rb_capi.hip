@@ -79,10 +79,11 @@ struct rb_world {
     int64_t N = 0, S = 0, Npad = 0, lo = 0;
     int32_t n_local = 0, P = 1, rank = 0;
     int32_t n_planes = 0, oriented = 1, maxp = 16, maxrec = 0;
-    // owned bodies up to which the cooperative search is used: above ~20k
-    // the wide form is faster (24k: 16.5 vs 15.9 us, 31k: 19.3 vs 16.1 us;
-    // 16k: 11.5 vs 14.4 us the other way)
-    int64_t coop_max = 20480;
+    // owned bodies up to which the cooperative search is used: above it
+    // the wide form (with its helper wave) is faster (19,600: 14.4 vs 12.1
+    // us; 16,384: 11.1 vs 11.3, 12,100: 10.4 vs 11.5 the other way;
+    // profiles/r03/wide_help/ab_thresh_flat.txt)
+    int64_t coop_max = 16384;
     int64_t wide_max = 65536;   // above coop_max, up to which the wide one-lane form is used
     // owned bodies up to which the cooperative form runs with a helper wave
     // per workgroup (inv(I_w), gravity and plane contacts off the body
