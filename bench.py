@@ -92,6 +92,13 @@ def parse():
     return ap.parse_args()
 
 
+# per-config World arguments: C4's rows slide into pile-ups after ~550 steps
+# with up to 28 sphere partners on a body; a synchronous
+# rb_step grows max_partners itself (guarded chunks), the bench's
+# graph-replayed steps cannot, so the timed C4 run starts at 32
+WORLD_KW = {"c4": {"max_partners": 32}}
+
+
 def make_scene(cfg: str, P: int, scaling: str):
     """The scene all ranks step together, and its description."""
     from rbhip import scenes
@@ -225,8 +232,9 @@ class SingleWorldCheck:
     whole scene stepped on rank 0's GPU (collective: every rank calls it
     with the same step count)."""
 
-    def __init__(self, scene, dtype, device, rank, P):
+    def __init__(self, scene, dtype, device, rank, P, kw=None):
         self.scene, self.dtype, self.device, self.rank, self.P = scene, dtype, device, rank, P
+        self.kw = kw or {}
         self.ref, self.done = None, 0
 
     def __call__(self, sw, steps_total) -> bool:
@@ -249,7 +257,7 @@ class SingleWorldCheck:
         if self.rank == 0:
             import rbhip
             if self.ref is None:
-                self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype)
+                self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype, **self.kw)
             self.ref.step(steps_total - self.done)
             self.done = steps_total
             q1, v1 = self.ref.get_state()
@@ -322,7 +330,7 @@ def main():
     from rbhip.shard import ShardedWorld
 
     scene, desc = make_scene(args.config, P, args.scaling)
-    check = SingleWorldCheck(scene, args.dtype, device, rank, P) if P > 1 else None
+    check = SingleWorldCheck(scene, args.dtype, device, rank, P, WORLD_KW.get(args.config)) if P > 1 else None
     dev_red = f"cuda:{device}" if backend == "nccl" else "cpu"
 
     def probe_ms(sw) -> float:
@@ -343,7 +351,7 @@ def main():
     PROBE = 20
     done = args.warmup
     if P == 1:
-        sw = ShardedWorld(scene, dtype=args.dtype, device=device)
+        sw = ShardedWorld(scene, dtype=args.dtype, device=device, **WORLD_KW.get(args.config, {}))
         sw.step(args.warmup)
         probes = {}
     else:
@@ -352,7 +360,8 @@ def main():
         for tr, halo in (("p2p", True), ("p2p", False), ("rccl", "auto"), ("nccl", False)):
             if tr in ("rccl", "nccl") and cands:
                 break
-            c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo)
+            c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo,
+                             **WORLD_KW.get(args.config, {}))
             name = c.transport + (" halo" if c.halo else " full reads" if c.transport == "p2p" else "")
             c.step(args.warmup)
             if not check(c, args.warmup):
