@@ -84,7 +84,12 @@ struct rb_world {
     // us; 16,384: 11.1 vs 11.3, 12,100: 10.4 vs 11.5 the other way;
     // profiles/r03/wide_help/ab_thresh_flat.txt)
     int64_t coop_max = 16384;
-    int64_t wide_max = 65536;   // above coop_max, up to which the wide one-lane form is used
+    // above coop_max, up to which the wide one-lane form is used; with its
+    // helper wave it is at least as fast as the one-lane form at every size
+    // measured (131k / 262k equal, 524k 0.116 -> 0.102 ms, 1M 0.236 ->
+    // 0.216, 4M 0.876 -> 0.841; profiles/r03/wide_help/ab_large2.txt), so
+    // the one-lane form only runs on request (RBHIP_WIDE_MAX_BODIES)
+    int64_t wide_max = INT64_MAX;
     // owned bodies up to which the cooperative form runs with a helper wave
     // per workgroup (inv(I_w), gravity and plane contacts off the body
     // lanes' chain): 4k 8.1 -> 7.4 us, 8k 9.6 -> 8.6; 16k 11.0 -> 11.9 the
