@@ -302,7 +302,7 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 #define RB_STAT_TILE_RESTART  5   /* blocks rebuilt at horizon 1               */
 #define RB_STAT_TILE_FALLBACK 6   /* runs finished on the per-step kernels     */
 #define RB_STAT_TILE_STEPS    7   /* steps committed by tile blocks            */
-#define RB_STAT_FORM          8   /* per-step kernel form (0 one-lane, 1 cooperative, 2 wide, 3 cooperative + helper) */
+#define RB_STAT_FORM          8   /* per-step kernel form (0 one-lane, 1 cooperative, 2 wide, 3 cooperative + helper, 4 wide + helper) */
 #define RB_STAT_TILES         9   /* tiles of the grid                         */
 #define RB_STAT_TILE_THREADS 10   /* threads (stepped bodies) per tile         */
 #define RB_STAT_TILE_KMAX    11

@@ -39,7 +39,7 @@ def run_one(sc):
         if os.environ.get("GRAPH", "1") == "1":
             # K graph-replayed steps between HIP events on torch's stream
             w.set_stream(torch.cuda.current_stream().cuda_stream)
-            w.step(60)
+            w.step(int(os.environ.get("WARM", "60")))
             w.step(200)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
