@@ -396,12 +396,12 @@ def main():
     ev0.record()                      # the library enqueues on torch's current stream
     sw.step(args.steps)
     ev1.record()
+    # rb_sync inside the clock: it reads the error word and finishes any work
+    # the library resolves at a sync point (a rolled-back / continued chunk),
+    # so every one of the K steps is complete and checked before the clock stops
+    sw.sync()
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    # the library's error word (a device-to-host copy and a stream sync) is
-    # read after the clock stops: the K steps are complete once the device
-    # synchronize returns, and a raised error still fails the run here
-    sw.sync()
     region_ms = ev0.elapsed_time(ev1)
     st1 = w.stats()
     tiled = st1.get("tile_steps", 0) > st0.get("tile_steps", 0)

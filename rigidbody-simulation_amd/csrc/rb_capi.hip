@@ -116,6 +116,7 @@ struct rb_world {
     bool fit_valid = false;        // fit_period: the group box (and layout) the last fit was made for
     int64_t fit_key[7] = {};
     int64_t bytes_per_body_step = 0;
+    std::vector<double> bound;     // host copy of every body's bounding radius (rb_set_state's snapshot rows)
     // device memory
     void *snap[2] = {};        // [Npad] Snap<T>: (x, y, z, bound radius), ping-pong
     void *qsnap[2] = {};       // boxes: [Npad][4] step-start orientations, ping-pong with snap
@@ -881,13 +882,16 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     while (left > 0) {
         int64_t K = left > chunk_max ? chunk_max : left;
         bool opt = w->boxes && w->box_opt && !sharded && w->P == 1 && w->box_skip == 0;
+        // a chunk run with the box kernel because of an earlier roll-back
+        // counts down the back-off (guarded or not)
+        const bool skipped = w->boxes && w->box_opt && !sharded && w->P == 1 && w->box_skip > 0;
+        if (skipped) --w->box_skip;
         // a guarded chunk can be rolled back: optimistic box chunks, and long
         // chunks of a synchronous call (rb_step), whose broadphase layout is
         // refitted if the scene drifted out of it (a bucket overflowed)
         const bool guard = opt || (w->sync_call && K >= GUARD_MIN_STEPS && !sharded && w->P == 1 &&
                                    w->law == RB_LAW_MUJOCO);
         if (!guard) {
-            if (w->box_skip > 0) --w->box_skip;
             if (int rc = replay(K, variant)) return rc;
             w->c += K;
             left -= K;
@@ -1060,9 +1064,6 @@ void free_world(rb_world *w) {
     if (w->cap_stream) (void)hipStreamDestroy(w->cap_stream);
     delete w;
 }
-
-// host-side copy of the bounding radii (needed by rb_set_state)
-std::map<const rb_world *, std::vector<double>> g_bounds;
 
 }  // namespace
 
@@ -1271,7 +1272,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     std::vector<double> bound;
     int rc = w->dtype == RB_F64 ? upload_consts<double>(w, d, bound) : upload_consts<float>(w, d, bound);
     if (rc) return bail(rc);
-    g_bounds[w] = std::move(bound);
+    w->bound = std::move(bound);
     *out = w;
     return RB_OK;
 }
@@ -1281,12 +1282,16 @@ void rb_world_destroy(rb_world *w) {
         (void)hipSetDevice(w->device);
         (void)hipStreamSynchronize(w->stream);
     }
-    g_bounds.erase(w);
     free_world(w);
 }
 
 int rb_set_stream(rb_world *w, void *s) {
     if (!w) return fail(RB_EINVAL, "null world");
+    HIPCHK(hipSetDevice(w->device));
+    // work queued on the old stream (a tile run's continuation included)
+    // finishes there before later work is ordered on the new one
+    if (int rc = tile_finish(w)) return rc;
+    HIPCHK(hipStreamSynchronize(w->stream));
     w->stream = (hipStream_t)s;        // NULL = HIP's null stream
     return RB_OK;
 }
@@ -1514,9 +1519,8 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     if (int rc = tile_finish(w)) return rc;
     fit_period(w, qpos);
     if (int rc = fit_tiles(w, qpos)) return rc;
-    const std::vector<double> &bound = g_bounds[w];
-    int rc = w->dtype == RB_F64 ? upload_state<double>(w, qpos, qvel, bound.data())
-                                : upload_state<float>(w, qpos, qvel, bound.data());
+    int rc = w->dtype == RB_F64 ? upload_state<double>(w, qpos, qvel, w->bound.data())
+                                : upload_state<float>(w, qpos, qvel, w->bound.data());
     w->primed = false;
     return rc;
 }

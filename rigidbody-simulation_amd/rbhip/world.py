@@ -52,8 +52,11 @@ class World:
         self._h = h
         self._L = L
         # records per body (rb_world_create): 4 per plane, 1 per sphere
-        # partner, up to 4 per partner in scenes with boxes
-        self.maxrec = 4 * d.n_planes + (4 if bool(np.any(self._kind != 0)) else 1) * max_partners
+        # partner, up to 4 per partner in scenes with boxes; max_partners can
+        # grow in a guarded chunk (16 -> 32), so contacts() recomputes it
+        self._n_planes = d.n_planes
+        self._any_box = bool(np.any(self._kind != 0))
+        self.maxrec = self._maxrec(max_partners)
         n_owned, bpb = C.c_int64(), C.c_int64()
         _lib.check(L.rb_query(h, C.byref(n_owned), C.byref(bpb)), "rb_query")
         self.n_owned = n_owned.value
@@ -65,6 +68,9 @@ class World:
         if law != "mujoco":
             self.set_contact_law(law, tol)
         self.set_state(scene.qpos0, scene.qvel0)
+
+    def _maxrec(self, max_partners: int) -> int:
+        return 4 * self._n_planes + (4 if self._any_box else 1) * max_partners
 
     def set_contact_law(self, law: str, tol: float = 0.01):
         """Switch between the default law and the two-ball law (rb_set_contact_law)."""
@@ -199,6 +205,7 @@ class World:
         """Contact list of the most recent step, CSR over owned bodies:
         (counts, partner, kind, dist)."""
         n = self.n_owned
+        self.maxrec = self._maxrec(self.stats()["max_partners"])   # (the library may have grown it)
         cap = max(1, n * self.maxrec)
         cnt = np.zeros(n, np.int32)
         par = np.zeros(cap, np.int32)
