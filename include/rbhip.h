@@ -315,7 +315,13 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 #define RB_STAT_TABLE_GROWS  18   /* of which with the bucket table doubled */
 #define RB_STAT_BUCKETS      19   /* buckets per table now */
 #define RB_STAT_MAX_PARTNERS 20   /* max_partners now (16 -> 32 after an overflow in a guarded chunk) */
-#define RB_STATS_COUNT       21
+#define RB_STAT_XB_RUNS      21   /* rb_step calls that ran XCD-resident K-step blocks */
+#define RB_STAT_XB_LAUNCHES  22   /* block launches enqueued                 */
+#define RB_STAT_XB_STEPS     23   /* steps committed by blocks (checked)     */
+#define RB_STAT_XB_FALLBACKS 24   /* block runs rolled back and replayed per step */
+#define RB_STAT_XB_K         25   /* steps per block launch                  */
+#define RB_STAT_XB_ON        26   /* a long rb_step would use the blocks now */
+#define RB_STATS_COUNT       27
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <map>
 #include <string>
 #include <tuple>
@@ -201,6 +202,31 @@ struct rb_world {
     int64_t tile_stats[8] = {};    // runs, blocks, redo (taint), redo (bound), restarts, fallbacks, steps, capacity refits
     bool tile_cap_grow = false;    // a run stopped on a tile's capacity: refit with more room
     double tile_room = 1.1;        // growth allowance of the fullest tile's band (raised by each capacity stop)
+    // XCD-resident K-step blocks (rb_xblock.hip): sphere worlds
+    // of the wide form on one rank
+    int xb_mode = -1;              // -1 auto, 0 off, 1 on (RBHIP_XB)
+    int xb_k = 8;                  // steps per launch (RBHIP_XB_K)
+    int xb_wpg = 0;                // workgroups per group (CUs / 8; 0: the device cannot run the blocks)
+    int64_t xb_min_bodies = 32768; // auto mode: fewer bodies step with the per-step kernels
+    int32_t xb_cap = 0;            // local bodies per group
+    int xb_axis = 0;               // slab axis
+    double xb_cut[XB_GROUPS + 1] = {};
+    bool xb_cut_valid = false;
+    double xb_valpha = 1.5, xb_vbeta = 0.5;   // speed bound of a launch (m/s): valpha max|v| + vbeta + K |g| dt
+    void *xb_sp = nullptr;         // [XB_GROUPS][4] StepParams<T> (device)
+    std::vector<char> xb_sp_host;  // the last upload (skipped when unchanged)
+    int32_t *xb_map = nullptr, *xb_lkind = nullptr;
+    void *xb_lsnap = nullptr, *xb_lstate = nullptr, *xb_lconst = nullptr;
+    uint32_t *xb_lines = nullptr;  // [XB_GROUPS][2][H][32] the groups' bucket tables
+    uint32_t *xb_spill = nullptr;  // [XB_GROUPS][2][2 + 2 SPILL_CAP]
+    int64_t xb_H = 0;              // buckets of those tables
+    XbCtl *xb_ctl = nullptr;
+    bool xb_pending = false;       // a run awaits its check (xb_finish)
+    int64_t xb_c0 = 0, xb_n = 0;
+    double xb_prm[4] = {};
+    int64_t xb_stats[4] = {};      // runs, launches, steps committed, runs rolled back and replayed per step
+    int32_t xb_backoff = 0;        // eligible runs to skip after a roll-back (doubles)
+    int32_t xb_skip = 0;
     // kernel timing
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
@@ -645,7 +671,7 @@ int tile_start(rb_world *w, int64_t n, double dt, double e, double mu, double th
 }
 
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false,
-                  bool allow_tile = true);
+                  bool allow_tile = true, bool allow_xb = true);
 int tile_refit(rb_world *w);
 
 // Wait for the run in flight; continue it if redos used up the spare blocks;
@@ -684,6 +710,13 @@ int tile_finish(rb_world *w) {
         return tile_refit(w);
     }
     return RB_OK;
+}
+
+int xb_finish(rb_world *w);
+// every run that awaits its check at the next sync point: tile runs, block runs
+int finish_pending(rb_world *w) {
+    if (int rc = tile_finish(w)) return rc;
+    return xb_finish(w);
 }
 
 // Guarded chunks (enqueue_steps): the chunk-start copy (state rows,
@@ -801,9 +834,296 @@ int refit_from_device(rb_world *w) {
     return RB_OK;
 }
 
+
+// ---- captured step graphs ---------------------------------------------------
+// A sequence of launches covering K steps from step c0 (`seq(stream, c0)`),
+// captured once per start parity and replayed (rb_world::graphs, keyed by the
+// step count, parity, step parameters and variant).
+int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, double mu, double thr,
+                 const std::function<int(hipStream_t, int64_t)> &seq) {
+    auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
+    auto it = w->graphs.find(key);
+    if (it == w->graphs.end()) {
+        evict_graphs(w, 2);
+        // capture both parities at once, so later calls starting at either
+        // replay without a capture (a parity still cached is kept; both
+        // entries get the current tick, so the one not launched now is not
+        // the first evicted)
+        for (int c0 = 0; c0 < 2; ++c0) {
+            const auto k0 = std::make_tuple(K, c0, dt, e, mu, thr, variant);
+            auto old = w->graphs.find(k0);
+            if (old != w->graphs.end()) { old->second.used = w->graph_tick; continue; }
+            hipGraph_t graph;
+            hipGraphExec_t ex;
+            HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
+            if (int rc = seq(w->cap_stream, c0)) { (void)hipStreamEndCapture(w->cap_stream, &graph); return rc; }
+            HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
+            HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+            (void)hipGraphDestroy(graph);
+            w->graphs[k0] = rb_world::GraphEntry{ex, w->graph_tick};
+        }
+        it = w->graphs.find(key);
+    }
+    it->second.used = ++w->graph_tick;
+    HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
+    return RB_OK;
+}
+
+// ---- XCD-resident K-step blocks (rb_xblock.hip) ----------------
+bool xb_eligible(const rb_world *w, int64_t nsteps) {
+    if (w->xb_mode == 0 || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
+        return false;
+    if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;
+    const int form = step_form(w);
+    if (form != FORM_WIDE && form != FORM_WIDE_HELP) return false;   // the block runs the wide form's body code
+    if (nsteps < 2) return false;
+    return w->xb_mode == 1 || w->N >= w->xb_min_bodies;
+}
+
+// the slabs: equal body counts along the widest horizontal axis (x, y) of
+// the positions qpos (stride 7); group g owns [cut[g], cut[g+1])
+void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride) {
+    w->xb_cut_valid = false;
+    if (w->N < XB_GROUPS) return;
+    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
+    for (int64_t b = 0; b < w->N; ++b)
+        for (int d = 0; d < 2; ++d) {
+            const double u = qpos[stride * b + d];
+            if (!(u == u) || fabs(u) > 1e12) return;     // (non-finite: the per-step kernels report it)
+            lo[d] = std::min(lo[d], u);
+            hi[d] = std::max(hi[d], u);
+        }
+    w->xb_axis = (hi[1] - lo[1]) > (hi[0] - lo[0]) ? 1 : 0;
+    std::vector<double> u((size_t)w->N);
+    for (int64_t b = 0; b < w->N; ++b) u[(size_t)b] = qpos[stride * b + w->xb_axis];
+    w->xb_cut[0] = -INFINITY;
+    w->xb_cut[XB_GROUPS] = INFINITY;
+    for (int g = 1; g < XB_GROUPS; ++g) {
+        const size_t k = (size_t)((int64_t)w->N * g / XB_GROUPS);
+        std::nth_element(u.begin(), u.begin() + k, u.end());
+        const double below = *std::max_element(u.begin(), u.begin() + k);
+        w->xb_cut[g] = 0.5 * (below + u[k]);
+    }
+    w->xb_cut_valid = true;
+}
+
+// the slabs fitted to the positions of the current step (the snapshot)
+int xb_refit_cuts(rb_world *w) {
+    std::vector<double> q((size_t)7 * w->N, 0.0);
+    const size_t ne = (size_t)4 * w->N;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    if (w->dtype == RB_F64) {
+        std::vector<double> sn(ne);
+        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sizeof(double) * ne, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; }
+    } else {
+        std::vector<float> sn(ne);
+        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sizeof(float) * ne, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; }
+    }
+    double old[XB_GROUPS + 1];
+    memcpy(old, w->xb_cut, sizeof old);
+    const int old_axis = w->xb_axis;
+    xb_fit_cuts(w, q.data(), 7);
+    if (memcmp(old, w->xb_cut, sizeof old) != 0 || old_axis != w->xb_axis)
+        drop_graphs(w);                                  // the cuts are captured kernel arguments
+    return RB_OK;
+}
+
+// the groups' buffers (lazily, at the first eligible run; the tables again
+// when the world's table size changes)
+int xb_alloc(rb_world *w) {
+    if (w->xb_ctl && w->xb_H == w->H) return RB_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);
+    if (!w->xb_ctl) {
+        // one group per XCD, one workgroup per CU
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, w->device));
+        w->xb_wpg = (cus % XB_GROUPS == 0 && cus / XB_GROUPS >= 1 && cus / XB_GROUPS <= XB_MAX_WPG) ? cus / XB_GROUPS : 0;
+        if (!w->xb_wpg) return RB_OK;
+        // room for the slab and a band of up to half its width on each side
+        // (a wider copy fails the block: the chunk replays step by step)
+        int64_t cap = std::min<int64_t>(w->N, 2 * ((w->N + XB_GROUPS - 1) / XB_GROUPS) + 8192);
+        cap = (cap + 63) / 64 * 64;
+        w->xb_cap = (int32_t)cap;
+        const size_t esz = (size_t)w->esz;
+        HIPCHK(hipMalloc((void **)&w->xb_map, sizeof(int32_t) * XB_GROUPS * cap));
+        HIPCHK(hipMalloc((void **)&w->xb_lkind, sizeof(int32_t) * XB_GROUPS * cap));
+        HIPCHK(hipMalloc(&w->xb_lsnap, esz * 4 * 2 * XB_GROUPS * cap));
+        HIPCHK(hipMalloc(&w->xb_lstate, esz * 13 * XB_GROUPS * cap));
+        HIPCHK(hipMalloc(&w->xb_lconst, esz * 8 * XB_GROUPS * cap));
+        HIPCHK(hipMalloc((void **)&w->xb_spill, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
+        HIPCHK(hipMemset(w->xb_spill, 0, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
+        HIPCHK(hipMalloc((void **)&w->xb_ctl, sizeof(XbCtl)));
+        HIPCHK(hipMemset(w->xb_ctl, 0, sizeof(XbCtl)));
+        const size_t spb = (w->dtype == RB_F64 ? sizeof(StepParams<double>) : sizeof(StepParams<float>)) * XB_GROUPS * 4;
+        HIPCHK(hipMalloc(&w->xb_sp, spb));
+    }
+    // the tables: generation-tagged like the world's (nothing is cleared), so
+    // a fresh allocation is zeroed and every group starts at generation 2
+    if (w->xb_lines) { HIPCHK(hipFree(w->xb_lines)); w->xb_lines = nullptr; }
+    const size_t words = (size_t)XB_GROUPS * 2 * LINE_WORDS * (size_t)w->H;
+    HIPCHK(hipMalloc((void **)&w->xb_lines, sizeof(uint32_t) * words));
+    HIPCHK(hipMemset(w->xb_lines, 0, sizeof(uint32_t) * words));
+    HIPCHK(hipMemset(w->xb_spill, 0, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
+    std::vector<uint32_t> gen((size_t)XB_GROUPS * 32, 2u);
+    HIPCHK(hipMemcpy(w->xb_ctl->gen, gen.data(), sizeof(uint32_t) * gen.size(), hipMemcpyHostToDevice));
+    w->xb_H = w->H;
+    w->xb_sp_host.clear();
+    return RB_OK;
+}
+
+// the groups' step parameters: [g][v], v = parity | (last step ? 2 : 0);
+// uploaded when they change (step parameters, the grid)
+template <typename T> int xb_upload_params(rb_world *w, double dt, double e, double mu, double thr) {
+    std::vector<StepParams<T>> sp((size_t)XB_GROUPS * 4);
+    const int64_t cap = w->xb_cap;
+    for (int g = 0; g < XB_GROUPS; ++g)
+        for (int v = 0; v < 4; ++v) {
+            const int par = v & 1;
+            StepParams<T> p = make_step<T>(w, 0, dt, e, mu, thr, true);
+            Snap<T> *ls = dp<Snap<T>>(w->xb_lsnap, 0) + (int64_t)g * 2 * cap;
+            p.snap_cur = ls + par * cap;
+            p.snap_next = ls + (1 - par) * cap;
+            p.st = BodyState<T>{dp<T>(w->xb_lstate, 0) + (int64_t)g * 13 * cap, cap};
+            p.cs = BodyConsts<T>{dp<T>(w->xb_lconst, 0) + (int64_t)g * 8 * cap, cap, w->xb_lkind + (int64_t)g * cap};
+            p.n_local = (int32_t)cap;
+            p.lo = 0;
+            p.n_global = cap;
+            p.S = (int32_t)cap;
+            p.xfrc = nullptr;
+            auto tab = [&](int q) {
+                return Table<T>{w->xb_lines + ((size_t)(2 * g + q) * LINE_WORDS * (size_t)w->H), nullptr, nullptr,
+                                w->xb_spill + (size_t)(2 * g + q) * (2 + 2 * SPILL_CAP)};
+            };
+            p.cur = tab(par);
+            p.next = v >= 2 ? Table<T>{nullptr, nullptr, nullptr, nullptr} : tab(1 - par);
+            p.epoch = nullptr;
+            p.bounds = nullptr;
+            p.plist = nullptr;
+            p.plist_cnt = nullptr;
+            p.rec_count = nullptr; p.rec_partner = nullptr; p.rec_kind = nullptr; p.rec_dist = nullptr;
+            p.maxrec = 0;
+            p.quat_cur = nullptr; p.quat_next = nullptr;
+            p.defer_q = nullptr; p.defer_cnt = nullptr; p.defer_reset = nullptr;
+            p.vel_cur = nullptr; p.vel_next = nullptr;
+            sp[(size_t)(4 * g + v)] = p;
+        }
+    const size_t bytes = sizeof(StepParams<T>) * sp.size();
+    if (w->xb_sp_host.size() == bytes && memcmp(w->xb_sp_host.data(), sp.data(), bytes) == 0) return RB_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    HIPCHK(hipMemcpy(w->xb_sp, sp.data(), bytes, hipMemcpyHostToDevice));
+    w->xb_sp_host.assign(reinterpret_cast<const char *>(sp.data()), reinterpret_cast<const char *>(sp.data()) + bytes);
+    return RB_OK;
+}
+
+template <typename T> XbParams<T> make_xb(rb_world *w, int64_t c, int K, double dt) {
+    XbParams<T> p{};
+    p.sp = static_cast<const StepParams<T> *>(w->xb_sp);
+    p.snap_in = dp<Snap<T>>(w->snap[c % 2], 0);
+    p.snap_out = dp<Snap<T>>(w->snap[(c + K) % 2], 0);
+    p.st_base = dp<T>(w->state, 0);
+    p.S = w->S;
+    p.cs = BodyConsts<T>{dp<T>(w->consts, 0), w->Npad, w->kind};
+    p.n = (int32_t)w->N;
+    p.axis = w->xb_axis;
+    for (int g = 0; g <= XB_GROUPS; ++g) p.cut[g] = (T)w->xb_cut[g];
+    p.K = K;
+    p.wpg = w->xb_wpg;
+    p.cap = w->xb_cap;
+    p.reach = (T)(2.0 * w->rmax);
+    p.gdt = (T)(sqrt(w->g[0] * w->g[0] + w->g[1] * w->g[1] + w->g[2] * w->g[2]) * dt);
+    p.valpha = (T)w->xb_valpha;
+    p.vbeta = (T)w->xb_vbeta;
+    p.map = w->xb_map;
+    p.lsnap = dp<Snap<T>>(w->xb_lsnap, 0);
+    p.lstate = dp<T>(w->xb_lstate, 0);
+    p.lconst = dp<T>(w->xb_lconst, 0);
+    p.lkind = w->xb_lkind;
+    p.ctl = w->xb_ctl;
+    p.err = w->err;
+    p.timeout_ticks = 50000000;        // 0.5 s at 100 MHz
+    return p;
+}
+
+// the launches of n block steps from step c0 on stream s: xb_k steps each
+int xb_enqueue(rb_world *w, hipStream_t s, int64_t c0, int64_t n, double dt) {
+    for (int64_t done = 0; done < n;) {
+        const int K = (int)std::min<int64_t>(w->xb_k, n - done);
+        const hipError_t r = w->dtype == RB_F64 ? launch_xblock<double>(make_xb<double>(w, c0 + done, K, dt), w->maxp, s)
+                                                : launch_xblock<float>(make_xb<float>(w, c0 + done, K, dt), w->maxp, s);
+        HIPCHK(r);
+        done += K;
+    }
+    return RB_OK;
+}
+
+// A run of n steps in blocks: the chunk-start state is saved (the blocks
+// commit in place), the launches replay from a graph, and the run is checked
+// at the next sync point (xb_finish; at once for a synchronous rb_step).
+int xb_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
+    if (int rc = xb_alloc(w)) return rc;
+    if (!w->xb_cut_valid)
+        if (int rc = xb_refit_cuts(w)) return rc;
+    if (!w->xb_wpg || !w->xb_cut_valid) {
+        if (!w->xb_wpg) w->xb_mode = 0;      // the device cannot run the blocks
+        return enqueue_steps(w, n, dt, e, mu, thr, false, false, false);
+    }
+    int rc = w->dtype == RB_F64 ? xb_upload_params<double>(w, dt, e, mu, thr) : xb_upload_params<float>(w, dt, e, mu, thr);
+    if (rc) return rc;
+    if ((rc = chunk_save(w))) return rc;
+    rc = graph_replay(w, n, 8, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) { return xb_enqueue(w, s, c0, n, dt); });
+    if (rc) return rc;
+    w->xb_pending = true;
+    w->xb_c0 = w->c;
+    w->xb_n = n;
+    w->xb_prm[0] = dt; w->xb_prm[1] = e; w->xb_prm[2] = mu; w->xb_prm[3] = thr;
+    w->c += n;
+    w->primed = false;                       // the world's own table is stale
+    w->xb_stats[0] += 1;
+    w->xb_stats[1] += (n + w->xb_k - 1) / w->xb_k;
+    if (w->sync_call) return xb_finish(w);
+    return RB_OK;
+}
+
+// The check of a block run: any error raised during it (ERR_XB: an
+// assumption of the blocks failed; or any other bit) rolls the chunk back
+// to its start and replays it with the per-step kernels, which report real
+// errors themselves.  After a roll-back the next eligible runs step per step
+// (a doubling back-off); a capacity failure refits the slabs to the current
+// positions, a placement or time-out failure turns the blocks off.
+int xb_finish(rb_world *w) {
+    if (!w->xb_pending) return RB_OK;
+    w->xb_pending = false;
+    int32_t err = 0;
+    bool deferred = false;
+    if (int rc = chunk_check(w, err, deferred)) return rc;
+    if (!err) {
+        w->xb_stats[2] += w->xb_n;
+        if (w->xb_backoff > 0) w->xb_backoff /= 2;
+        return RB_OK;
+    }
+    w->xb_stats[3] += 1;
+    XbCtl ctl;
+    HIPCHK(hipMemcpy(&ctl, w->xb_ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    // barrier counters and the poison word back to a clean start (the
+    // generations stay: they only grow)
+    HIPCHK(hipMemset(w->xb_ctl, 0, offsetof(XbCtl, cnt)));
+    HIPCHK(hipMemset(&w->xb_ctl->poison, 0, 2 * sizeof(int32_t)));
+    if (ctl.why & (XB_WHY_PLACEMENT | XB_WHY_TIMEOUT)) w->xb_mode = 0;
+    w->xb_backoff = w->xb_backoff ? std::min(2 * w->xb_backoff, 64) : 1;
+    w->xb_skip = w->xb_backoff;
+    w->c = w->xb_c0;
+    if (int rc = chunk_restore(w)) return rc;
+    if (ctl.why & XB_WHY_CAP) w->xb_cut_valid = false;   // the slabs drifted: refit at the next run
+    const double *q = w->xb_prm;
+    return enqueue_steps(w, w->xb_n, q[0], q[1], q[2], q[3], false, false, false);
+}
+
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded,
-                  bool allow_tile) {
+                  bool allow_tile, bool allow_xb) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
     if (!sharded && w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_run or rb_shard_step + exchange");
     if (sharded && !w->comm && !w->p2p) return fail(RB_EINVAL, "rb_shard_run before rb_shard_comm_init or rb_p2p_connect");
@@ -812,13 +1132,23 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     if (!sharded && allow_tile && tile_eligible(w, nsteps)) {
         int rc = tile_start(w, w->record ? nsteps - 1 : nsteps, dt, e, mu, thr);
         if (rc || !w->record) return rc;
         // the recorded (last) step runs on the per-step kernels
-        if ((rc = tile_finish(w))) return rc;
+        if ((rc = finish_pending(w))) return rc;
         nsteps = 1;
+    } else if (!sharded && allow_xb && xb_eligible(w, w->record ? nsteps - 1 : nsteps)) {
+        if (w->xb_skip > 0) {
+            --w->xb_skip;                        // (back-off after a roll-back: this run steps per step)
+        } else {
+            int rc = xb_run(w, w->record ? nsteps - 1 : nsteps, dt, e, mu, thr);
+            if (rc || !w->record) return rc;
+            // the recorded (last) step runs on the per-step kernels
+            if ((rc = finish_pending(w))) return rc;
+            nsteps = 1;
+        }
     }
     if (int rc = gen_guard(w, nsteps)) return rc;
     if (!w->primed || (w->law == RB_LAW_BALLS && (dt != w->prm_dt || e != w->prm_e || mu != w->prm_mu))) {
@@ -846,35 +1176,11 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     }
     // K > 1: replay a captured graph of K step nodes
     auto replay = [&](int64_t K, int variant) -> int {
-        auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
-        auto it = w->graphs.find(key);
-        if (it == w->graphs.end()) {
-            evict_graphs(w, 2);
-            // capture both parities at once, so later calls starting at
-            // either replay without a capture (a parity still cached is
-            // kept; both entries get the current tick, so the one not
-            // launched now is not the first evicted)
-            for (int c0 = 0; c0 < 2; ++c0) {
-                const auto k0 = std::make_tuple(K, c0, dt, e, mu, thr, variant);
-                auto old = w->graphs.find(k0);
-                if (old != w->graphs.end()) { old->second.used = w->graph_tick; continue; }
-                hipGraph_t graph;
-                hipGraphExec_t ex;
-                HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
-                for (int64_t k = 0; k < K; ++k) {
-                    int rc = one(w->cap_stream, c0 + k);
-                    if (rc) { (void)hipStreamEndCapture(w->cap_stream, &graph); return rc; }
-                }
-                HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
-                HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
-                (void)hipGraphDestroy(graph);
-                w->graphs[k0] = rb_world::GraphEntry{ex, w->graph_tick};
-            }
-            it = w->graphs.find(key);
-        }
-        it->second.used = ++w->graph_tick;
-        HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
-        return RB_OK;
+        return graph_replay(w, K, variant, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) {
+            for (int64_t k = 0; k < K; ++k)
+                if (int rc = one(s, c0 + k)) return rc;
+            return (int)RB_OK;
+        });
     };
     const int variant = (int)w->record | (sharded ? 2 : 0);
     const int64_t chunk_max = 512;
@@ -1049,7 +1355,8 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *tbufs[] = {w->tile_rec, w->tile_count, w->tile_ctl, w->opt_save};
+    void *tbufs[] = {w->tile_rec, w->tile_count, w->tile_ctl, w->opt_save, w->xb_sp, w->xb_map, w->xb_lkind, w->xb_lsnap,
+                     w->xb_lstate, w->xb_lconst, w->xb_lines, w->xb_spill, w->xb_ctl};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_ctl_host) (void)hipHostFree(w->tile_ctl_host);
@@ -1132,6 +1439,13 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // K-step tile blocks (rb_tile.hip): RBHIP_TILE = 0 off, 1 on, unset auto
     // (sphere worlds of >= RBHIP_TILE_MIN_BODIES on one rank)
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) ? 1 : 0;
+    // XCD-resident K-step blocks (rb_xblock.hip): RBHIP_XB = 0 off, 1 on,
+    // unset auto (sphere worlds of the wide form, >= RBHIP_XB_MIN_BODIES)
+    if (const char *ev = getenv("RBHIP_XB")) w->xb_mode = atoi(ev) ? 1 : 0;
+    if (const char *ev = getenv("RBHIP_XB_K")) w->xb_k = std::max(1, std::min(64, atoi(ev)));
+    if (const char *ev = getenv("RBHIP_XB_MIN_BODIES")) w->xb_min_bodies = atoll(ev);
+    if (const char *ev = getenv("RBHIP_XB_VALPHA")) w->xb_valpha = atof(ev);
+    if (const char *ev = getenv("RBHIP_XB_VBETA")) w->xb_vbeta = atof(ev);
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     if (const char *ev = getenv("RBHIP_TILE_K")) w->tile_kmax = std::max(1, std::min(64, atoi(ev)));
@@ -1278,7 +1592,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
 }
 
 void rb_world_destroy(rb_world *w) {
-    if (w && w->tile_pending) {
+    if (w && (w->tile_pending || w->xb_pending)) {
         (void)hipSetDevice(w->device);
         (void)hipStreamSynchronize(w->stream);
     }
@@ -1290,7 +1604,7 @@ int rb_set_stream(rb_world *w, void *s) {
     HIPCHK(hipSetDevice(w->device));
     // work queued on the old stream (a tile run's continuation included)
     // finishes there before later work is ordered on the new one
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     HIPCHK(hipStreamSynchronize(w->stream));
     w->stream = (hipStream_t)s;        // NULL = HIP's null stream
     return RB_OK;
@@ -1516,9 +1830,10 @@ static int fit_tiles(rb_world *w, const double *qpos) {
 int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     if (!w || !qpos || !qvel) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     fit_period(w, qpos);
     if (int rc = fit_tiles(w, qpos)) return rc;
+    w->xb_cut_valid = false;                             // block slabs: refitted at the next block run
     int rc = w->dtype == RB_F64 ? upload_state<double>(w, qpos, qvel, w->bound.data())
                                 : upload_state<float>(w, qpos, qvel, w->bound.data());
     w->primed = false;
@@ -1528,14 +1843,14 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
 int rb_get_state(rb_world *w, double *qpos, double *qvel) {
     if (!w || (!qpos && !qvel)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     return w->dtype == RB_F64 ? download_state<double>(w, qpos, qvel) : download_state<float>(w, qpos, qvel);
 }
 
 int rb_set_xfrc(rb_world *w, const double *xf) {
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     drop_graphs(w);
     if (!xf) {
         if (w->xfrc) { HIPCHK(hipFree(w->xfrc)); w->xfrc = nullptr; }
@@ -1562,7 +1877,7 @@ int rb_step_async(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
 int rb_sync(rb_world *w) {
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     return read_err(w);
 }
 
@@ -1571,7 +1886,7 @@ int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double 
     int rc = rb_step_async(w, nsteps, dt, e, mu, thr);
     if (w) w->sync_call = false;
     if (rc) return rc;
-    if ((rc = tile_finish(w))) return rc;
+    if ((rc = finish_pending(w))) return rc;
     return read_err(w);
 }
 
@@ -1756,7 +2071,7 @@ int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double e, double mu, do
 int rb_record_contacts(rb_world *w, int enable) {
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     if (enable && !w->rec_count) {
         const size_t slots = (size_t)w->maxrec * (w->S > 0 ? w->S : 1);
         HIPCHK(hipMalloc((void **)&w->rec_count, sizeof(int32_t) * w->S));
@@ -1775,7 +2090,7 @@ int rb_get_contacts(rb_world *w, int32_t *counts, int32_t *partner, int32_t *kin
     if (!w || !counts) return fail(RB_EINVAL, "null argument");
     if (!w->rec_count) return fail(RB_EINVAL, "contact recording was never enabled");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     const size_t slots = (size_t)w->maxrec * w->S;
     std::vector<int32_t> c((size_t)w->S), pa(slots), ki(slots);
     std::vector<double> di(slots);
@@ -1869,7 +2184,7 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
             return fail(RB_EUNSUPPORTED, "the two-ball law's only plane is the z = 0 ground (ball_collision.py:88-90)");
     }
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     HIPCHK(hipStreamSynchronize(w->stream));
     if (law == RB_LAW_BALLS && !w->vel[0]) {
         const size_t bytes = (size_t)w->esz * 8 * w->Npad;
@@ -1938,7 +2253,7 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
     if (mode < -1 || mode > 1 || kmax < 0 || kmax > 64 || !(band >= 0) || owned < 0)
         return fail(RB_EINVAL, "bad tile configuration");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     w->tile_mode = mode;
     if (kmax) w->tile_kmax = kmax;
     if (band > 0) w->tile_band = band;
@@ -1950,14 +2265,15 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
-    if (int rc = tile_finish(w)) return rc;
+    if (int rc = finish_pending(w)) return rc;
     const int form = step_form(w);
     const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), w->tile_stats[0], w->tile_stats[1], w->tile_stats[2],
                                        w->tile_stats[3], w->tile_stats[4], w->tile_stats[5], w->tile_stats[6],
                                        form, (int64_t)w->tile_ntx * w->tile_nty, w->tile_nt, w->tile_kmax, w->tile_cap,
                                        (int64_t)(w->tile_size * 1e6), tile_eligible(w, 1 << 20) ? 1 : 0,
                                        w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H,
-                                       (int64_t)w->maxp};
+                                       (int64_t)w->maxp, w->xb_stats[0], w->xb_stats[1], w->xb_stats[2], w->xb_stats[3],
+                                       (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

@@ -60,6 +60,52 @@ __device__ __forceinline__ int64_t chk(int64_t idx, int64_t n, int line) {
 }
 #define CHK(idx, n) chk((idx), (n), __LINE__)
 
+// Loads of data another workgroup of the SAME launch may have written (the
+// step-start snapshot, bucket heads and slots, the spill list): plain loads
+// in the per-step kernels, whose writers are all in the previous launch.  In
+// the XCD-resident block kernel (rb_xblock.hip, RB_XB) the steps follow each
+// other inside one launch, separated by a barrier among the workgroups of one
+// XCD: there they must bypass the CU's vector L1, which is never refreshed by
+// another CU's stores, and are served by the XCD's L2, which every writer
+// shares (MI355X_MICROARCH.md, inter-workgroup visibility; scripts/xb_probe.hip).
+#ifndef RB_XB
+#define RB_XB 0
+#endif
+// XCD-resident loads: 1 = sc1 (agent-scope relaxed atomic loads, 8 bytes
+// each), 2 = nt 16-byte loads
+#ifndef RB_XB_LD
+#define RB_XB_LD 1
+#endif
+template <typename V> __device__ __forceinline__ V xld(const V *p) {
+#if RB_XB
+    static_assert(sizeof(V) % 4 == 0, "xld: whole words");
+    V v;
+    if constexpr (RB_XB_LD == 2 && sizeof(V) % 16 == 0) {
+        using u4 = __attribute__((ext_vector_type(4))) unsigned;
+        u4 t[sizeof(V) / 16];
+#pragma unroll
+        for (size_t k = 0; k < sizeof(V) / 16; ++k) t[k] = __builtin_nontemporal_load(reinterpret_cast<const u4 *>(p) + k);
+        __builtin_memcpy(&v, t, sizeof(V));
+    } else if constexpr (sizeof(V) % 8 == 0) {
+        unsigned long long t[sizeof(V) / 8];
+#pragma unroll
+        for (size_t k = 0; k < sizeof(V) / 8; ++k)
+            t[k] = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p) + k, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_memcpy(&v, t, sizeof(V));
+    } else {
+        unsigned t[sizeof(V) / 4];
+#pragma unroll
+        for (size_t k = 0; k < sizeof(V) / 4; ++k)
+            t[k] = __hip_atomic_load(reinterpret_cast<const unsigned *>(p) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_memcpy(&v, t, sizeof(V));
+    }
+    return v;
+#else
+    return *p;
+#endif
+}
+
 constexpr uint32_t N_XCD = 8;
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 #if RB_XCD_REMAP
@@ -251,12 +297,12 @@ __device__ __forceinline__ void spill_insert(const Table<T> &tab, int32_t *err, 
 template <typename T, typename F>
 __device__ __forceinline__ void spill_scan(const Table<T> &tab, uint32_t gen, uint32_t b, F f) {
     if (!tab.spill) return;
-    const uint2 h = *reinterpret_cast<const uint2 *>(tab.spill);
+    const uint2 h = xld(reinterpret_cast<const uint2 *>(tab.spill));
     const int32_t n = h.y != gen ? 0 : h.x < (uint32_t)SPILL_CAP ? (int32_t)h.x : SPILL_CAP;
     const uint2 *e = reinterpret_cast<const uint2 *>(tab.spill + 2);
 #pragma unroll 1
     for (int32_t k = 0; k < n; ++k) {
-        const uint2 v = e[k];
+        const uint2 v = xld(e + k);
         if (v.x == b) f(v.y);
     }
 }
@@ -294,14 +340,14 @@ __device__ __forceinline__ void insert_id(const Grid<T> &g, const Table<T> &tab,
 // the header carries the table's generation (clamped to the slots).
 template <typename T>
 __device__ __forceinline__ uint4 bucket_head(const Table<T> &tab, uint32_t b, int rl) {
-    return *reinterpret_cast<const uint4 *>(head_words(tab, b, rl));
+    return xld(reinterpret_cast<const uint4 *>(head_words(tab, b, rl)));
 }
 __device__ __forceinline__ int32_t head_count(const uint4 &h, uint32_t gen) {
     return h.y != gen ? 0 : h.x < (uint32_t)BUCKET_SLOTS ? (int32_t)h.x : BUCKET_SLOTS;
 }
 template <typename T>
 __device__ __forceinline__ uint32_t bucket_id(const Table<T> &tab, uint32_t b, const uint4 &h, int s, int rl) {
-    return s == 0 ? h.z : s == 1 ? h.w : *slot_word(tab, b, s, rl);
+    return s == 0 ? h.z : s == 1 ? h.w : xld(slot_word(tab, b, s, rl));
 }
 
 // The 2x2x2 cell neighbourhood: cell size = 2 x the largest contact reach
@@ -392,7 +438,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
                 }
                 rem -= c[k];
             }
-            if (base + u < total && at) t = *at;
+            if (base + u < total && at) t = xld(at);
             tj[u] = (base + u < total) ? t : (uint32_t)i;
         }
         // the id-indexed snapshot: ids are spatially coherent, so a wave's
@@ -403,7 +449,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
         for (int u = 0; u < RB_QBATCH; ++u) {
             sn[u] = Snap<T>{RB_ABLATE == 5 ? x.x + T(1000) : x.x, x.y, x.z, T(0)};
             if ((tj[u] & ~BOX_FLAG) != (uint32_t)i && RB_ABLATE != 5)
-                sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+                sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
         }
 #pragma unroll
         for (int u = 0; u < RB_QBATCH; ++u)
@@ -419,7 +465,7 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
             spill_scan(p.cur, gen, b[k], [&](uint32_t t) {
                 const uint32_t j = t & ~BOX_FLAG;
                 if (j == (uint32_t)i) return;
-                if (hit(t, p.snap_cur[CHK(j, p.n_global)])) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)j, overflow);
+                if (hit(t, xld(p.snap_cur + CHK(j, p.n_global)))) list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)j, overflow);
             });
         }
     }
@@ -477,7 +523,7 @@ struct Head6 { uint4 a, b; };
 template <typename T>
 __device__ __forceinline__ Head6 bucket_head6(const Table<T> &tab, uint32_t b, int rl) {
     const uint4 *l = reinterpret_cast<const uint4 *>(head_words(tab, b, rl));
-    return Head6{l[0], l[1]};
+    return Head6{xld(l), xld(l + 1)};
 }
 template <int S> __device__ __forceinline__ uint32_t head6_id(const Head6 &h) {
     static_assert(S >= 0 && S < WIDE_HEAD_IDS, "head slot");
@@ -553,7 +599,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
             sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
-            if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+            if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
         }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
@@ -585,11 +631,11 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 Snap<T> sn[QB];
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
-                    tj[u] = s0 + u < ck ? *slot_word(p.cur, bk, s0 + u, rl) : (uint32_t)i;
+                    tj[u] = s0 + u < ck ? xld(slot_word(p.cur, bk, s0 + u, rl)) : (uint32_t)i;
 #pragma unroll
                 for (int u = 0; u < QB; ++u) {
                     sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
-                    if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = p.snap_cur[CHK(tj[u] & ~BOX_FLAG, p.n_global)];
+                    if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
                 }
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
@@ -609,7 +655,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
             spill_scan(p.cur, gen, s_cand[k * NB + tid], [&](uint32_t t) {
                 const uint32_t j = t & ~BOX_FLAG;
                 if (j == (uint32_t)i) return;
-                const Snap<T> sn = p.snap_cur[CHK(j, p.n_global)];
+                const Snap<T> sn = xld(p.snap_cur + CHK(j, p.n_global));
                 if (!hit(t, sn)) return;
                 if (RB_WIDE_LDSPOS) list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)j, sn, overflow);
                 else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)j, overflow);

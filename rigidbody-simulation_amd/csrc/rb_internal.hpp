@@ -323,6 +323,63 @@ template <typename T> struct TileParams {
     int64_t c0;                        // step counter at the start of the run
 };
 
+// ---- XCD-resident K-step blocks (rb_xblock.hip) -----------------
+// One launch steps the scene K times.  Its workgroups form XB_GROUPS groups
+// (blocks b, b + 8, b + 16, ... : the workgroups of one XCD, checked against
+// the XCC_ID register), one per slab of the scene along its widest horizontal
+// axis.  Each group copies its slab's bodies plus a ghost band wide enough
+// that no body outside the copy can influence an owned body within K steps
+// into buffers of its own, rebuilds its own broadphase table every step, and
+// steps the copy K times — separated by barriers among the group's
+// workgroups only, so the copy, its snapshots and its tables stay in that
+// XCD's L2 — before writing its owned bodies back.
+constexpr int XB_GROUPS = 8;
+constexpr int XB_THREADS = 512;        // one workgroup per CU: 8 waves, 2 per SIMD
+constexpr int XB_MAX_WPG = 64;         // workgroups per group at most
+constexpr int32_t ERR_XB = 1 << 21;    // an assumption of a block failed (speed bound, capacity, placement,
+                                       // barrier time-out): the host rolls the chunk back and replays it with
+                                       // the per-step kernels (never user-visible)
+struct XbCtl {
+    unsigned long long bar[XB_GROUPS][16];   // group barrier arrivals, one 128-B line per group (monotone)
+    unsigned long long gathered[16];         // workgroups done gathering (monotone, every group)
+    int32_t cnt[XB_GROUPS][XB_MAX_WPG];      // loaded bodies in each workgroup's id chunk
+    uint32_t vpart[XB_GROUPS][XB_MAX_WPG];   // float bits: max |v| over each workgroup's id chunk
+    uint32_t gen[XB_GROUPS][32];             // the group's next table generation
+    uint32_t xcc[XB_GROUPS * XB_MAX_WPG];    // XCC id of each workgroup
+    int32_t poison;                          // a wait timed out: later waits are skipped
+    int32_t why;                             // XB_WHY_* bits of the failures since the last reset
+    int32_t pad0[30];
+    int32_t nload[XB_GROUPS];                // loaded bodies of each group (statistics, last launch)
+    uint32_t vmax_bits;                      // float bits: max |v| at the start of the last launch (statistics)
+};
+enum : int32_t { XB_WHY_SPEED = 1, XB_WHY_CAP = 2, XB_WHY_PLACEMENT = 4, XB_WHY_TIMEOUT = 8 };
+template <typename T> struct XbParams {
+    const StepParams<T> *sp;           // [XB_GROUPS][4]: the group's step parameters, (parity, last step)
+    const Snap<T> *snap_in;            // the scene at step c (global ids)
+    Snap<T> *snap_out;                 // the owned bodies at step c + K (== snap_in when K is even)
+    T *st_base;                        // state rows [13][S] (global ids; P == 1), in place
+    int64_t S;
+    BodyConsts<T> cs;
+    int32_t n;                         // bodies
+    int32_t axis;                      // slab axis: 0 x, 1 y
+    T cut[XB_GROUPS + 1];              // group g owns axis coordinate in [cut[g], cut[g+1]) (first / last open)
+    int32_t K;                         // steps of this launch
+    int32_t wpg;                       // workgroups per group
+    int32_t cap;                       // local bodies per group at most
+    T reach;                           // contact reach: 2 x the largest radius
+    T gdt;                             // |g| dt
+    T valpha, vbeta;                   // speed bound of a launch: valpha max|v| + vbeta + K |g| dt
+    int32_t *map;                      // [XB_GROUPS][cap] local index -> global id (ascending)
+    Snap<T> *lsnap;                    // [XB_GROUPS][2][cap] the copy's snapshots, ping-pong
+    T *lstate;                         // [XB_GROUPS][13][cap]
+    T *lconst;                         // [XB_GROUPS][8][cap]
+    int32_t *lkind;                    // [XB_GROUPS][cap]
+    XbCtl *ctl;
+    int32_t *err;
+    int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) a wait may take
+};
+template <typename T> hipError_t launch_xblock(const XbParams<T> &p, int maxp, hipStream_t s);
+
 // launchers (rb_tile.hip)
 template <typename T> hipError_t launch_tile_gather(const TileParams<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_tile_block(const TileParams<T> &p, int nt, hipStream_t s);

@@ -422,9 +422,9 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                 pe[u] = ppos[(s0 + u) * stride];
             } else if constexpr (PM == 2) {
                 const int d = pdidx[(s0 + u) * stride];
-                pe[u] = d < WIDE_HPOS ? ppos[d * stride] : p.snap_cur[CHK(jj[u], p.n_global)];
+                pe[u] = d < WIDE_HPOS ? ppos[d * stride] : xld(p.snap_cur + CHK(jj[u], p.n_global));
             } else {
-                pe[u] = p.snap_cur[CHK(jj[u], p.n_global)];
+                pe[u] = xld(p.snap_cur + CHK(jj[u], p.n_global));
             }
         }
 #pragma unroll
@@ -540,7 +540,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
     const int32_t i = ld.lo + l;
 
     // ---- K1 first: the contact search reads only step-start data -----------
-    const Snap<T> self = ld.snap_cur[i];
+    const Snap<T> self = xld(ld.snap_cur + i);
     const V3<T> x = {self.x, self.y, self.z};
     const int32_t ci = RB_ABLATE == 8 ? 0 : i;    // (diagnostic, load_body)
     const int32_t kind = ld.cs.kind[ci];
