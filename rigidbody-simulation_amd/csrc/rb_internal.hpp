@@ -394,6 +394,21 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
 // the wide form's kernel alone (its own translation unit: scheduled for memory clauses)
 template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, bool help, hipStream_t s);
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s);
+// rb_set_state / rb_get_state on the device: the reference's AoS rows (qpos
+// stride 7: x y z qw qx qy qz; qvel stride 6: v, w; multi_sphere_bounce.py:85-88)
+// <-> the SoA state rows and the snapshot (rb_kernels.hip)
+template <typename T> struct StateIO {
+    double *qpos, *qvel;               // [N][7], [N][6] (device; rows [lo, lo + n_local) for the state)
+    Snap<T> *snap;                     // the current snapshot (every body)
+    T *quat;                           // box worlds: the current orientation snapshot, else nullptr
+    BodyState<T> st;
+    const T *bound;                    // [Npad] bounding radii
+    int64_t N, lo;
+    int32_t n_local;
+    int32_t balls;                     // two-ball law: positions are the state's px py pz (the snapshot is post-ground)
+};
+template <typename T> hipError_t launch_state_in(const StateIO<T> &p, hipStream_t s);
+template <typename T> hipError_t launch_state_out(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);

@@ -1107,6 +1107,67 @@ template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, i
     return hipGetLastError();
 }
 
+// ---- the state across the boundary (rb_set_state / rb_get_state) ----------
+// One lane per body: AoS rows of the caller (qpos[7k], qvel[6k], D1-fixed
+// multi_sphere_bounce.py layout) <-> SoA state rows and snapshot.  The host
+// moves the rows with one DMA each way (pinned staging, rb_capi.hip).
+template <typename T>
+__global__ __launch_bounds__(256) void state_in_kernel(StateIO<T> p) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.N) return;
+    const double *q = p.qpos + 7 * b;
+    p.snap[b] = Snap<T>{(T)q[0], (T)q[1], (T)q[2], p.bound[b]};
+    if (p.quat) {
+        T *o = p.quat + 4 * b;
+        o[0] = (T)q[3]; o[1] = (T)q[4]; o[2] = (T)q[5]; o[3] = (T)q[6];
+    }
+    const int64_t l = b - p.lo;
+    if (l < 0 || l >= p.n_local) return;
+    const double *v = p.qvel + 6 * b;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) p.st.row(d)[l] = (T)q[3 + d];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) p.st.row(4 + d)[l] = (T)v[d];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) p.st.row(10 + d)[l] = (T)q[d];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void state_out_kernel(StateIO<T> p, int want_q, int want_v) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= p.n_local) return;
+    const int64_t b = p.lo + l;
+    if (want_q) {
+        double *q = p.qpos + 7 * b;
+        if (p.balls) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) q[d] = (double)p.st.row(10 + d)[l];
+        } else {
+            const Snap<T> s = p.snap[b];
+            q[0] = (double)s.x; q[1] = (double)s.y; q[2] = (double)s.z;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) q[3 + d] = (double)p.st.row(d)[l];
+    }
+    if (want_v) {
+        double *v = p.qvel + 6 * b;
+#pragma unroll
+        for (int d = 0; d < 6; ++d) v[d] = (double)p.st.row(4 + d)[l];
+    }
+}
+
+template <typename T> hipError_t launch_state_in(const StateIO<T> &p, hipStream_t s) {
+    if (p.N <= 0) return hipSuccess;
+    hipLaunchKernelGGL((state_in_kernel<T>), dim3((unsigned)((p.N + 255) / 256)), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+template <typename T> hipError_t launch_state_out(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s) {
+    if (p.n_local <= 0) return hipSuccess;
+    hipLaunchKernelGGL((state_out_kernel<T>), dim3((unsigned)((p.n_local + 255) / 256)), dim3(256), 0, s, p,
+                       want_q ? 1 : 0, want_v ? 1 : 0);
+    return hipGetLastError();
+}
+
 template <typename T> hipError_t launch_insert(const InsertParams<T> &p, hipStream_t s) {
     if (p.count <= 0) return hipSuccess;
     const int64_t blocks = (p.count + 255) / 256;
@@ -1171,6 +1232,8 @@ template hipError_t launch_step_wide<float>(const StepParams<float> &, int, bool
 template hipError_t launch_step<double>(const StepParams<double> &, int, int, bool, hipStream_t);
 template hipError_t launch_kat_narrow<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
+template hipError_t launch_state_in<double>(const StateIO<double> &, hipStream_t);
+template hipError_t launch_state_out<double>(const StateIO<double> &, bool, bool, hipStream_t);
 template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
@@ -1179,6 +1242,8 @@ template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, 
 template hipError_t launch_step<float>(const StepParams<float> &, int, int, bool, hipStream_t);
 template hipError_t launch_kat_narrow<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
+template hipError_t launch_state_in<float>(const StateIO<float> &, hipStream_t);
+template hipError_t launch_state_out<float>(const StateIO<float> &, bool, bool, hipStream_t);
 template hipError_t launch_kat_impulse<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);
