@@ -274,10 +274,13 @@ class SingleWorldCheck:
         return bool(int(t.item()))
 
 
-def step_kernel_name(stats: dict, tiled: bool) -> str:
+def step_kernel_name(stats: dict, tiled: bool, blocked: bool = False) -> str:
     """The kernel that stepped the timed region, as the library reports it
-    (rb_world_stats): the tile-block kernel, or the per-step form."""
+    (rb_world_stats): the XCD-resident block kernel, the tile-block kernel,
+    or the per-step form."""
     from rbhip import _lib
+    if blocked:
+        return "rb::xblock_kernel"
     if tiled:
         return "rb::tile_block_kernel"
     return _lib.FORM_NAMES.get(stats.get("form"), "?")
@@ -405,6 +408,9 @@ def main():
     region_ms = ev0.elapsed_time(ev1)
     st1 = w.stats()
     tiled = st1.get("tile_steps", 0) > st0.get("tile_steps", 0)
+    # XCD-resident K-step blocks (rb_xblock.hip): every timed step committed
+    # by blocks, none rolled back
+    blocked = st1.get("xb_steps", 0) - st0.get("xb_steps", 0) == args.steps
     timed = [done + args.steps + 1, done + 2 * args.steps]
     if P > 1:
         t = torch.tensor([elapsed], device=dev_red, dtype=torch.float64)
@@ -417,7 +423,14 @@ def main():
     # region is exactly K back-to-back step-kernel launches (graph replay),
     # so HIP events around it / K.  Several ranks: a step also runs the
     # exchange, so time each step-kernel launch with its own event pair.
-    if P == 1 and tiled:
+    if P == 1 and blocked:
+        # one launch steps K reference steps: the timed region is exactly the
+        # run's block launches, so its HIP-event time / K steps is the time
+        # per step (rocprofv3's per-launch average / K agrees)
+        avg_ms, launches = region_ms / args.steps, st1["xb_launches"] - st0["xb_launches"]
+        timing = ("HIP events around the timed region / K steps (XCD-resident blocks of xb_k steps per launch: "
+                  "achieved = algorithmic bytes of the K steps / region time)")
+    elif P == 1 and tiled:
         # K-step tile blocks: one launch steps up to kmax reference steps;
         # the timed region is the run's launches (gather, blocks, write-back)
         avg_ms, launches = region_ms / args.steps, st1["tile_blocks"] - st0["tile_blocks"]
@@ -464,13 +477,18 @@ def main():
                      "traffic_source": traffic_src,
                      # the counters were collected on this very library build
                      "traffic_same_build": traffic_same_build,
-                     "kernel": step_kernel_name(st1, tiled),
+                     "kernel": step_kernel_name(st1, tiled, blocked),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
-    if tiled:
+    if blocked or tiled:
         line["roofline"]["algorithmic_bytes_per_launch"] = None
+        line["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
+    if blocked:
+        line["xblock"] = {"steps_per_launch": st1["xb_k"],
+                          **{k: st1[k] - st0[k] for k in ("xb_runs", "xb_launches", "xb_steps", "xb_fallbacks")}}
+    if tiled:
         line["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
         line["tile"] = {k: st1[k] - st0[k] for k in ("tile_blocks", "tile_redo_taint", "tile_redo_bound",
                                                       "tile_restart", "tile_fallback", "tile_steps")}

@@ -321,7 +321,9 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 #define RB_STAT_XB_FALLBACKS 24   /* block runs rolled back and replayed per step */
 #define RB_STAT_XB_K         25   /* steps per block launch                  */
 #define RB_STAT_XB_ON        26   /* a long rb_step would use the blocks now */
-#define RB_STATS_COUNT       27
+#define RB_STAT_IO_SKIPPED   27   /* rb_set_state calls that were no-ops (the bytes rb_get_state handed out) */
+#define RB_STAT_IO_UPLOADS   28   /* rb_set_state calls that uploaded          */
+#define RB_STATS_COUNT       29
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

@@ -886,7 +886,7 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
 bool xb_eligible(const rb_world *w, int64_t nsteps) {
     if (w->xb_mode == 0 || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
         return false;
-    if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;
+    if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;   // (N <= 16,384 x wpg)
     const int form = step_form(w);
     if (form != FORM_WIDE && form != FORM_WIDE_HELP) return false;   // the block runs the wide form's body code
     if (nsteps < 2) return false;
@@ -2381,7 +2381,7 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
                                        (int64_t)(w->tile_size * 1e6), tile_eligible(w, 1 << 20) ? 1 : 0,
                                        w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H,
                                        (int64_t)w->maxp, w->xb_stats[0], w->xb_stats[1], w->xb_stats[2], w->xb_stats[3],
-                                       (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0};
+                                       (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0, w->io_stats[0], w->io_stats[1]};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

@@ -482,6 +482,11 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
 #define RB_WIDE_LDSPOS 1
 #endif
 constexpr int WIDE_HPOS = 8;
+// the rare path (buckets of 7+ bodies) software-pipelined over its batches
+// (0: each batch's ids, then its snapshots)
+#ifndef RB_WIDE_PIPE
+#define RB_WIDE_PIPE 1
+#endif
 // diagnostic (0): the wide search skips buckets' ids past the head (wrong
 // for a bucket of 7+ bodies); measures the rare path's code footprint
 #ifndef RB_WIDE_MORE
@@ -621,6 +626,61 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
             s_cand[k * NB + tid] = b[k];
             s_cand[(8 + k) * NB + tid] = (uint32_t)c[k];
         }
+        auto test = [&](const uint32_t (&tj)[QB], const Snap<T> (&sn)[QB], int s0, int32_t ck) {
+#pragma unroll
+            for (int u = 0; u < QB; ++u)
+                if (s0 + u < ck && hit(tj[u], sn[u])) {
+                    if (RB_WIDE_LDSPOS)
+                        list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u],
+                                              overflow);
+                    else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+                }
+        };
+        auto gather = [&](const uint32_t (&tj)[QB], Snap<T> (&sn)[QB]) {
+#pragma unroll
+            for (int u = 0; u < QB; ++u) {
+                sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
+                if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
+            }
+        };
+#if RB_WIDE_PIPE
+        // Software-pipelined over the (bucket, slot batch) sequence: the ids
+        // of the next batch load under the current batch's snapshots, so a
+        // crowded neighbourhood (C4's pile-ups: 8 buckets of ~30 ids) costs
+        // one dependent round trip per batch instead of two
+        int k = 0, s0 = WIDE_HEAD_IDS - QB;
+        auto next_batch = [&]() -> bool {        // (k, s0) <- the next batch with ids left
+            s0 += QB;
+            while (k < 8) {
+                if (s0 < (int32_t)s_cand[(8 + k) * NB + tid]) return true;
+                ++k;
+                s0 = WIDE_HEAD_IDS;
+            }
+            return false;
+        };
+        uint32_t tjn[QB];
+        auto load_ids = [&]() {
+            const uint32_t bk = s_cand[k * NB + tid];
+            const int32_t ck = (int32_t)s_cand[(8 + k) * NB + tid];
+#pragma unroll
+            for (int u = 0; u < QB; ++u) tjn[u] = s0 + u < ck ? xld(slot_word(p.cur, bk, s0 + u, rl)) : (uint32_t)i;
+        };
+        bool have = next_batch();
+        if (have) load_ids();
+#pragma unroll 1
+        while (have) {
+            uint32_t tj[QB];
+#pragma unroll
+            for (int u = 0; u < QB; ++u) tj[u] = tjn[u];
+            const int scur = s0;
+            const int32_t ccur = (int32_t)s_cand[(8 + k) * NB + tid];
+            Snap<T> sn[QB];
+            gather(tj, sn);
+            have = next_batch();
+            if (have) load_ids();
+            test(tj, sn, scur, ccur);
+        }
+#else
 #pragma unroll 1
         for (int k = 0; k < 8; ++k) {
             const uint32_t bk = s_cand[k * NB + tid];
@@ -632,21 +692,11 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
                 for (int u = 0; u < QB; ++u)
                     tj[u] = s0 + u < ck ? xld(slot_word(p.cur, bk, s0 + u, rl)) : (uint32_t)i;
-#pragma unroll
-                for (int u = 0; u < QB; ++u) {
-                    sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
-                    if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
-                }
-#pragma unroll
-                for (int u = 0; u < QB; ++u)
-                    if (s0 + u < ck && hit(tj[u], sn[u])) {
-                        if (RB_WIDE_LDSPOS)
-                            list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u],
-                                                  overflow);
-                        else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
-                    }
+                gather(tj, sn);
+                test(tj, sn, s0, ck);
             }
         }
+#endif
     }
     if (RB_WIDE_MORE && spm) {                        // rarer: ids past full buckets (a spilled
 #pragma unroll 1                                      // bucket is a 7+ one: its index is stashed)

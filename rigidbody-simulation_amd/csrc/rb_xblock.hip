@@ -47,6 +47,7 @@
 namespace rb {
 
 static_assert(STEP_BLOCK == XB_THREADS, "one body per lane of the block");
+constexpr int XB_CHUNK = 16384;        // ids a workgroup scans at most (the host checks N <= XB_CHUNK x wpg)
 
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 15; }
 
@@ -110,6 +111,7 @@ void xblock_kernel(XbParams<T> P) {
     __shared__ uint32_t s_cand[WIDE_MAXC * XB_THREADS];
     __shared__ uint8_t s_didx[1];
     __shared__ int s_w[XB_THREADS / 64];
+    __shared__ unsigned long long s_flag[XB_CHUNK / 64];   // the chunk's ids in the copy (one bit each)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = (int)(blockIdx.x % XB_GROUPS), r = (int)(blockIdx.x / XB_GROUPS), wpg = P.wpg;
     XbCtl *C = P.ctl;
@@ -156,12 +158,20 @@ void xblock_kernel(XbParams<T> P) {
     const T olo = g == 0 ? -INFINITY : P.cut[g], ohi = g == XB_GROUPS - 1 ? INFINITY : P.cut[g + 1];
     if (g == 0 && r == 0 && tid == 0) C->vmax_bits = __float_as_uint(vmax);
 
-    // ---- 2. the copy: this chunk's bodies within [lo, hi), counted
+    // ---- 2. the copy: this chunk's bodies within [lo, hi), flagged in LDS
+    // (one bit per id of the chunk) and counted
     int cnt = 0;
-    for (int id = c0 + tid; id < c1; id += XB_THREADS) {
-        const T u = axis_of(P.snap_in[id], P.axis);
-        if (!(u == u)) atomicOr(P.err, ERR_DOMAIN);
-        cnt += (u >= lo && u < hi) ? 1 : 0;
+    for (int b0 = c0; b0 < c1; b0 += XB_THREADS) {
+        const int id = b0 + tid;
+        bool in = false;
+        if (id < c1) {
+            const T u = axis_of(P.snap_in[id], P.axis);
+            if (!(u == u)) atomicOr(P.err, ERR_DOMAIN);
+            in = u >= lo && u < hi;
+        }
+        const unsigned long long m = __ballot(in);
+        if (lane == 0) s_flag[(b0 - c0) / 64 + wave] = m;
+        cnt += in ? 1 : 0;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
@@ -186,7 +196,8 @@ void xblock_kernel(XbParams<T> P) {
     if (fits) {
         for (int b0 = c0; b0 < c1; b0 += XB_THREADS) {
             const int id = b0 + tid;
-            const bool in = id < c1 && ([&] { const T u = axis_of(P.snap_in[id], P.axis); return u >= lo && u < hi; })();
+            const unsigned long long m = s_flag[(b0 - c0) / 64 + wave];
+            const bool in = (m >> lane) & 1ull;
             int t;
             const int o = block_scan(in ? 1 : 0, s_w, &t);
             if (in) map[off + o] = id;

@@ -82,7 +82,7 @@ STAT_NAMES = ["graphs", "tile_runs", "tile_blocks", "tile_redo_taint", "tile_red
               "tile_fallback", "tile_steps", "form", "tiles", "tile_threads", "tile_kmax", "tile_cap",
               "tile_size_um", "tile_on", "box_opt_chunks", "box_rollbacks", "refits",
               "table_grows", "buckets", "max_partners", "xb_runs", "xb_launches", "xb_steps",
-              "xb_fallbacks", "xb_k", "xb_on"]
+              "xb_fallbacks", "xb_k", "xb_on", "io_skipped", "io_uploads"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
               3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help"}
 

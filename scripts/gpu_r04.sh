@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-4 GPU session steps, run on the gpurun box from the repo root:
+#   scripts/gpu_r04.sh STEP [STEP ...]
+# Each step runs under its own time limit; a step that ends in anything but
+# success or test failures (rc 0 / 1: a fault, abort, segfault, time limit)
+# stops the session there.
+export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {   # name, seconds, command...
+    local name=$1 secs=$2; shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    tail -4 "gpurun_out/$name.log"
+    echo "== $name rc=$rc"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc $rc)"; exit $rc; fi
+    return 0
+}
+for step in "$@"; do
+    case $step in
+        xbtest) run xb_tests 600 python -u -m pytest tests/test_gpu_xblock.py -x -v --timeout 300 --timeout-method thread ;;
+        xbtime) run xb_time 300 python -u scripts/xb_time.py --ks 0,2,4,6,8,12 ;;
+        shims) run shims 300 python -u -m pytest tests/test_gpu_shims.py tests/test_gpu_threads.py -x -q --timeout 300 --timeout-method thread ;;
+        c4ab) LIBS="rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline SIZES=256x256 WARM=500 \
+              ENVS="RBHIP_XB=0" ROUNDS=2 run c4_pipe_ab 300 python -u scripts/ablate.py ;;
+        framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
+        pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
