@@ -274,15 +274,12 @@ class SingleWorldCheck:
         return bool(int(t.item()))
 
 
-def step_kernel_name(stats: dict, tiled: bool, blocked: bool = False) -> str:
+def step_kernel_name(stats: dict, blocked: bool = False) -> str:
     """The kernel that stepped the timed region, as the library reports it
-    (rb_world_stats): the XCD-resident block kernel, the tile-block kernel,
-    or the per-step form."""
+    (rb_world_stats): the XCD-resident block kernel, or the per-step form."""
     from rbhip import _lib
     if blocked:
         return "rb::xblock_kernel"
-    if tiled:
-        return "rb::tile_block_kernel"
     return _lib.FORM_NAMES.get(stats.get("form"), "?")
 
 
@@ -407,7 +404,6 @@ def main():
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
     st1 = w.stats()
-    tiled = st1.get("tile_steps", 0) > st0.get("tile_steps", 0)
     # XCD-resident K-step blocks (rb_xblock.hip): every timed step committed
     # by blocks, none rolled back
     blocked = st1.get("xb_steps", 0) - st0.get("xb_steps", 0) == args.steps
@@ -430,12 +426,6 @@ def main():
         avg_ms, launches = region_ms / args.steps, st1["xb_launches"] - st0["xb_launches"]
         timing = ("HIP events around the timed region / K steps (XCD-resident blocks of xb_k steps per launch: "
                   "achieved = algorithmic bytes of the K steps / region time)")
-    elif P == 1 and tiled:
-        # K-step tile blocks: one launch steps up to kmax reference steps;
-        # the timed region is the run's launches (gather, blocks, write-back)
-        avg_ms, launches = region_ms / args.steps, st1["tile_blocks"] - st0["tile_blocks"]
-        timing = ("HIP events around the timed region / K steps (tile blocks: achieved = algorithmic bytes of "
-                  "the K committed steps / region time)")
     elif P == 1:
         avg_ms, launches, timing = region_ms / args.steps, args.steps, "HIP events around the timed region / K"
     else:
@@ -477,23 +467,17 @@ def main():
                      "traffic_source": traffic_src,
                      # the counters were collected on this very library build
                      "traffic_same_build": traffic_same_build,
-                     "kernel": step_kernel_name(st1, tiled, blocked),
+                     "kernel": step_kernel_name(st1, blocked),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
-    if blocked or tiled:
+    if blocked:
         line["roofline"]["algorithmic_bytes_per_launch"] = None
         line["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
     if blocked:
         line["xblock"] = {"steps_per_launch": st1["xb_k"],
                           **{k: st1[k] - st0[k] for k in ("xb_runs", "xb_launches", "xb_steps", "xb_fallbacks")}}
-    if tiled:
-        line["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
-        line["tile"] = {k: st1[k] - st0[k] for k in ("tile_blocks", "tile_redo_taint", "tile_redo_bound",
-                                                      "tile_restart", "tile_fallback", "tile_steps")}
-        line["tile"].update({k: st1[k] for k in ("tiles", "tile_threads", "tile_kmax", "tile_cap")})
-        line["tile"]["tile_size_m"] = st1["tile_size_um"] * 1e-6
     if rank == 0 and P == 1 and not args.no_cpu_baseline:
         w.close()
         base, ref = cpu_baseline(args.config, args.cpu_steps)

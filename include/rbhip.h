@@ -280,20 +280,15 @@ int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in,
  * since the last reset (HIP events on the world's stream; enable first). */
 int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
 
-/* K-step tile blocks (no reference counterpart: the reference steps one
- * frame per call, multi_sphere_bounce.py:42).  Sphere worlds on one rank
- * step blocks of up to kmax reference steps per kernel launch: each tile of
- * the scene plus a ghost band of width `band` is stepped in on-chip memory,
- * and a block is committed only when it is provably identical to single
- * steps (else redone shorter) -- results are bit-identical either way.
- * mode -1 = auto (currently: off -- measured no faster than the per-step
- * kernels on the BASELINE scenes; env RBHIP_TILE overrides),
- * 0 = off, 1 = on; kmax / band (m) / owned (target bodies per tile): 0
- * keeps the current value.  Refits the tile grid to the current positions. */
+/* Retired in round 4: the LDS tile blocks of round 3.  Kept
+ * for ABI compatibility: mode -1 (auto) and 0 (off) are accepted and do
+ * nothing; mode 1 returns RB_EUNSUPPORTED.  Long runs of sphere worlds step
+ * in XCD-resident K-step blocks instead (RBHIP_XB; RB_STAT_XB_*). */
 int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned);
 
 /* Counters for tests and measurement; fills out[0 .. min(n, RB_STATS_COUNT))
- * and returns how many: */
+ * and returns how many (the RB_STAT_TILE* slots 1-7 and 9-14 read 0: the
+ * tile path was retired in round 4): */
 #define RB_STAT_GRAPHS        0   /* captured step graphs alive               */
 #define RB_STAT_TILE_RUNS     1   /* rb_step calls that ran tile blocks        */
 #define RB_STAT_TILE_BLOCKS   2   /* tile block launches that did work         */

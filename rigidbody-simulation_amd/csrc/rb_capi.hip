@@ -185,27 +185,6 @@ struct rb_world {
     struct GraphEntry { hipGraphExec_t ex; uint64_t used; };
     std::map<std::tuple<int64_t, int, double, double, double, double, int>, GraphEntry> graphs;
     uint64_t graph_tick = 0;
-    // K-step tile blocks (rb_tile.hip): sphere worlds, one rank
-    // Auto mode is off until a scene size where the blocks beat the per-step
-    // kernels is measured (C3 about parity, 8k and 1M bodies slower)
-    int tile_mode = -1;            // -1 auto (RBHIP_TILE), 0 off, 1 on
-    int tile_kmax = 8;             // longest block
-    double tile_band = 0;          // ghost band W (0: 10 x rmax)
-    int64_t tile_owned = 0;        // target owned bodies per tile (0: 160 in fp64, 256 in fp32)
-    int64_t tile_min_bodies = INT64_MAX;   // auto mode: fewer bodies step with the per-step kernels
-    int tile_nt = 512;             // threads (= stepped bodies) per tile workgroup (fp32: 768)
-    int32_t tile_ntx = 0, tile_nty = 0, tile_cap = 0;
-    double tile_ox = 0, tile_oy = 0, tile_size = 0;
-    void *tile_rec = nullptr;      // [2][ntile][cap] TileRec<T>
-    int32_t *tile_count = nullptr; // [2][ntile]
-    TileCtl *tile_ctl = nullptr;
-    TileCtl *tile_ctl_host = nullptr;   // pinned: [0] the run's initial control word, [1] read back
-    bool tile_pending = false;
-    int64_t tile_c0 = 0, tile_target = 0;
-    double tile_prm[4] = {};       // dt, e, mu, thr of the pending run
-    int64_t tile_stats[8] = {};    // runs, blocks, redo (taint), redo (bound), restarts, fallbacks, steps, capacity refits
-    bool tile_cap_grow = false;    // a run stopped on a tile's capacity: refit with more room
-    double tile_room = 1.1;        // growth allowance of the fullest tile's band (raised by each capacity stop)
     // XCD-resident K-step blocks (rb_xblock.hip): sphere worlds
     // of the wide form on one rank
     int xb_mode = -1;              // -1 auto, 0 off, 1 on (RBHIP_XB)
@@ -585,152 +564,12 @@ int gen_guard(rb_world *w, int64_t nsteps) {
     return RB_OK;
 }
 
-// ---- K-step tile blocks (rb_tile.hip) --------------------------
-// A run of n steps: the canonical state is binned by tile (gather), blocks of
-// up to tile_kmax steps run one launch each (the device decides each block's
-// length, commits or redoes it: TileCtl), and the committed state is written
-// back (scatter).  The host only checks at the end that every step was
-// committed; if the device stopped early (a capacity limit), the remaining
-// steps run on the per-step kernels from the committed state.
-
-bool tile_eligible(const rb_world *w, int64_t nsteps) {
-    if (w->tile_mode == 0 || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
-        return false;
-    if (w->tile_ntx <= 0 || !w->tile_rec) return false;
-    if (nsteps < (w->record ? 3 : 2)) return false;
-    return w->tile_mode == 1 || w->N >= w->tile_min_bodies;
-}
-
-template <typename T> TileParams<T> make_tile(rb_world *w, double dt, double e, double mu, double thr) {
-    TileParams<T> p{};
-    p.rec = reinterpret_cast<TileRec<T> *>(w->tile_rec);
-    p.count = w->tile_count;
-    p.ctl = w->tile_ctl;
-    p.ntx = w->tile_ntx;
-    p.nty = w->tile_nty;
-    p.ntile = w->tile_ntx * w->tile_nty;
-    p.cap = w->tile_cap;
-    p.ox = (T)w->tile_ox;
-    p.oy = (T)w->tile_oy;
-    p.tile = (T)w->tile_size;
-    p.band = (T)(w->tile_band > 0 ? w->tile_band : 10.0 * w->rmax);
-    p.rmax = (T)w->rmax;
-    p.cs.base = dp<T>(w->consts, 0);
-    p.cs.Npad = w->Npad;
-    p.cs.kind = w->kind;
-    p.n_planes = w->n_planes;
-    for (int k = 0; k < w->n_planes; ++k)
-        for (int d = 0; d < 3; ++d) { p.pn[k][d] = (T)w->planes[k][d]; p.pp[k][d] = (T)w->planes[k][3 + d]; }
-    for (int d = 0; d < 3; ++d) p.g[d] = (T)w->g[d];
-    p.dt = (T)dt; p.e = (T)e; p.mu = (T)mu; p.thr = (T)thr;
-    p.oriented = w->oriented;
-    p.kmax = w->tile_kmax;
-    p.err = w->err;
-    p.st_base = dp<T>(w->state, 0);
-    p.S = w->S;
-    p.lo = (int32_t)w->lo;
-    p.n_local = w->n_local;
-    p.snap_in = dp<Snap<T>>(w->snap[w->sp()], 0);
-    p.snap_out[0] = dp<Snap<T>>(w->snap[0], 0);
-    p.snap_out[1] = dp<Snap<T>>(w->snap[1], 0);
-    p.c0 = w->c;
-    return p;
-}
-
-// blocks (and the final write-back) of the run in flight
-int tile_enqueue_blocks(rb_world *w, int64_t blocks) {
-    const double *q = w->tile_prm;
-    hipError_t r = hipSuccess;
-    if (w->dtype == RB_F64) {
-        TileParams<double> p = make_tile<double>(w, q[0], q[1], q[2], q[3]);
-        p.c0 = w->tile_c0;
-        for (int64_t b = 0; b < blocks && r == hipSuccess; ++b) r = launch_tile_block<double>(p, w->tile_nt, w->stream);
-        if (r == hipSuccess) r = launch_tile_scatter<double>(p, w->stream);
-    } else {
-        TileParams<float> p = make_tile<float>(w, q[0], q[1], q[2], q[3]);
-        p.c0 = w->tile_c0;
-        for (int64_t b = 0; b < blocks && r == hipSuccess; ++b) r = launch_tile_block<float>(p, w->tile_nt, w->stream);
-        if (r == hipSuccess) r = launch_tile_scatter<float>(p, w->stream);
-    }
-    HIPCHK(r);
-    return RB_OK;
-}
-
-int tile_start(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
-    TileCtl &c = w->tile_ctl_host[0];
-    memset(&c, 0, sizeof c);
-    c.target = n;
-    c.k_s = c.k_plan = w->tile_kmax;
-    c.k_run = (int32_t)(n < w->tile_kmax ? n : w->tile_kmax);
-    c.acc_valid = 1 << 30;
-    const int64_t ntile = (int64_t)w->tile_ntx * w->tile_nty;
-    HIPCHK(hipMemcpyAsync(w->tile_ctl, &c, sizeof c, hipMemcpyHostToDevice, w->stream));
-    HIPCHK(hipMemsetAsync(w->tile_count, 0, sizeof(int32_t) * 2 * ntile, w->stream));
-    w->tile_prm[0] = dt; w->tile_prm[1] = e; w->tile_prm[2] = mu; w->tile_prm[3] = thr;
-    w->tile_c0 = w->c;
-    w->tile_target = n;
-    const hipError_t g = w->dtype == RB_F64 ? launch_tile_gather<double>(make_tile<double>(w, dt, e, mu, thr), w->stream)
-                                            : launch_tile_gather<float>(make_tile<float>(w, dt, e, mu, thr), w->stream);
-    HIPCHK(g);
-    // every block commits up to kmax steps; a few spare blocks absorb redos
-    // (a block with nothing left exits at once)
-    const int64_t k = w->tile_kmax;
-    if (int rc = tile_enqueue_blocks(w, (n + k - 1) / k + 1 + n / (8 * k))) return rc;
-    w->tile_pending = true;
-    w->c += n;
-    w->primed = false;                       // the broadphase table is stale
-    w->tile_stats[0] += 1;
-    return RB_OK;
-}
-
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false,
-                  bool allow_tile = true, bool allow_xb = true);
-int tile_refit(rb_world *w);
-
-// Wait for the run in flight; continue it if redos used up the spare blocks;
-// on a capacity stop, finish on the per-step kernels.
-int tile_finish(rb_world *w) {
-    if (!w->tile_pending) return RB_OK;
-    w->tile_pending = false;
-    TileCtl c{};
-    for (int iter = 0;; ++iter) {
-        HIPCHK(hipMemcpyAsync(&w->tile_ctl_host[1], w->tile_ctl, sizeof(TileCtl), hipMemcpyDeviceToHost, w->stream));
-        HIPCHK(hipStreamSynchronize(w->stream));
-        c = w->tile_ctl_host[1];
-        if (c.err || c.done >= c.target || iter >= 64) break;
-        const int64_t left = c.target - c.done, k = c.k_plan > 0 ? c.k_plan : 1;
-        if (int rc = tile_enqueue_blocks(w, (left + k - 1) / k + 1)) return rc;
-    }
-    w->tile_stats[1] += c.blocks;
-    w->tile_stats[2] += c.redo_taint;
-    w->tile_stats[3] += c.redo_disp;
-    w->tile_stats[4] += c.restart;
-    w->tile_stats[6] += c.done;
-    w->c = w->tile_c0 + c.done;
-    if (c.done >= w->tile_target) return RB_OK;
-    // the device stopped early (a tile's capacity, the band): the rest on the
-    // per-step kernels, from the committed state the write-back left
-    w->tile_stats[5] += 1;
-    const double *q = w->tile_prm;
-    int rc = enqueue_steps(w, w->tile_target - c.done, q[0], q[1], q[2], q[3], false, false);
-    if (rc) return rc;
-    if (c.err & ERR_TILE) {
-        // a tile outgrew its lanes or bins: refit to the positions now, with
-        // more room, before the next run
-        w->tile_cap_grow = true;
-        w->tile_room *= 1.25;
-        w->tile_stats[7] += 1;
-        return tile_refit(w);
-    }
-    return RB_OK;
-}
+                  bool allow_xb = true);
 
 int xb_finish(rb_world *w);
-// every run that awaits its check at the next sync point: tile runs, block runs
-int finish_pending(rb_world *w) {
-    if (int rc = tile_finish(w)) return rc;
-    return xb_finish(w);
-}
+// every run that awaits its check at the next sync point (block runs)
+int finish_pending(rb_world *w) { return xb_finish(w); }
 
 // Guarded chunks (enqueue_steps): the chunk-start copy (state rows,
 // snapshot, box orientations, error word), the check after the chunk (error
@@ -1081,7 +920,7 @@ int xb_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
         if (int rc = xb_refit_cuts(w)) return rc;
     if (!w->xb_wpg || !w->xb_cut_valid) {
         if (!w->xb_wpg) w->xb_mode = 0;      // the device cannot run the blocks
-        return enqueue_steps(w, n, dt, e, mu, thr, false, false, false);
+        return enqueue_steps(w, n, dt, e, mu, thr, false, false);
     }
     int rc = w->dtype == RB_F64 ? xb_upload_params<double>(w, dt, e, mu, thr) : xb_upload_params<float>(w, dt, e, mu, thr);
     if (rc) return rc;
@@ -1131,12 +970,12 @@ int xb_finish(rb_world *w) {
     if (int rc = chunk_restore(w)) return rc;
     if (ctl.why & XB_WHY_CAP) w->xb_cut_valid = false;   // the slabs drifted: refit at the next run
     const double *q = w->xb_prm;
-    return enqueue_steps(w, w->xb_n, q[0], q[1], q[2], q[3], false, false, false);
+    return enqueue_steps(w, w->xb_n, q[0], q[1], q[2], q[3], false, false);
 }
 
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded,
-                  bool allow_tile, bool allow_xb) {
+                  bool allow_xb) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
     if (!sharded && w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_run or rb_shard_step + exchange");
     if (sharded && !w->comm && !w->p2p) return fail(RB_EINVAL, "rb_shard_run before rb_shard_comm_init or rb_p2p_connect");
@@ -1147,13 +986,7 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     w->state_version += 1;
-    if (!sharded && allow_tile && tile_eligible(w, nsteps)) {
-        int rc = tile_start(w, w->record ? nsteps - 1 : nsteps, dt, e, mu, thr);
-        if (rc || !w->record) return rc;
-        // the recorded (last) step runs on the per-step kernels
-        if ((rc = finish_pending(w))) return rc;
-        nsteps = 1;
-    } else if (!sharded && allow_xb && xb_eligible(w, w->record ? nsteps - 1 : nsteps)) {
+    if (!sharded && allow_xb && xb_eligible(w, w->record ? nsteps - 1 : nsteps)) {
         if (w->xb_skip > 0) {
             --w->xb_skip;                        // (back-off after a roll-back: this run steps per step)
         } else {
@@ -1424,11 +1257,10 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *tbufs[] = {w->tile_rec, w->tile_count, w->tile_ctl, w->opt_save, w->xb_sp, w->xb_map, w->xb_lkind, w->xb_lsnap,
+    void *tbufs[] = {w->opt_save, w->xb_sp, w->xb_map, w->xb_lkind, w->xb_lsnap,
                      w->xb_lstate, w->xb_lconst, w->xb_lines, w->xb_spill, w->xb_ctl};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
-    if (w->tile_ctl_host) (void)hipHostFree(w->tile_ctl_host);
     if (w->defer_host) (void)hipHostFree(w->defer_host);
     if (w->io_q_h) (void)hipHostFree(w->io_q_h);
     if (w->io_v_h) (void)hipHostFree(w->io_v_h);
@@ -1509,9 +1341,6 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_HELP")) w->wide_help = atoi(ev) != 0;
-    // K-step tile blocks (rb_tile.hip): RBHIP_TILE = 0 off, 1 on, unset auto
-    // (sphere worlds of >= RBHIP_TILE_MIN_BODIES on one rank)
-    if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) ? 1 : 0;
     // XCD-resident K-step blocks (rb_xblock.hip): RBHIP_XB = 0 off, 1 on,
     // unset auto (sphere worlds of the wide form, >= RBHIP_XB_MIN_BODIES)
     if (const char *ev = getenv("RBHIP_XB")) w->xb_mode = atoi(ev) ? 1 : 0;
@@ -1521,10 +1350,6 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_XB_VBETA")) w->xb_vbeta = atof(ev);
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
-    if (const char *ev = getenv("RBHIP_TILE_K")) w->tile_kmax = std::max(1, std::min(64, atoi(ev)));
-    if (const char *ev = getenv("RBHIP_TILE_BAND")) w->tile_band = atof(ev);
-    if (const char *ev = getenv("RBHIP_TILE_OWNED")) w->tile_owned = std::max<int64_t>(16, atoll(ev));
-    if (const char *ev = getenv("RBHIP_TILE_MIN_BODIES")) w->tile_min_bodies = atoll(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
     // snapshot line per bucket) 16 per body; the one-lane and wide forms
     // (linear cell groups, below) 32 per body, so the groups' period spans
@@ -1665,7 +1490,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
 }
 
 void rb_world_destroy(rb_world *w) {
-    if (w && (w->tile_pending || w->xb_pending)) {
+    if (w && w->xb_pending) {
         (void)hipSetDevice(w->device);
         (void)hipStreamSynchronize(w->stream);
     }
@@ -1675,7 +1500,7 @@ void rb_world_destroy(rb_world *w) {
 int rb_set_stream(rb_world *w, void *s) {
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
-    // work queued on the old stream (a tile run's continuation included)
+    // work queued on the old stream (a block run's check included)
     // finishes there before later work is ordered on the new one
     if (int rc = finish_pending(w)) return rc;
     HIPCHK(hipStreamSynchronize(w->stream));
@@ -1820,86 +1645,6 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
     w->fit_key[6] = (int64_t)w->group;
 }
 
-// Tile grid of the K-step blocks (rb_tile.hip): square xy tiles sized for
-// ~tile_owned bodies each over the bodies' xy box, at least 2.5 bands wide
-// (a tile's 3 x 3 bins must hold its band and outer ring); bins with room
-// for twice the fullest tile.  Bodies that later leave the box fall into
-// the edge tiles (unbounded outward).
-static int fit_tiles(rb_world *w, const double *qpos) {
-    if (w->P != 1 || !w->all_spheres || w->tile_mode == 0) return RB_OK;
-    // auto mode allocates the bins only for scenes it would tile
-    if (w->tile_mode < 0 && w->N < w->tile_min_bodies) { w->tile_ntx = 0; return RB_OK; }
-    w->tile_nt = w->dtype == RB_F64 ? 512 : 768;
-    // RBHIP_TILE_NT=256 (fp64): small tiles, one wave per SIMD across the
-    // chip for small scenes (a strong-scaling shard)
-    if (const char *ev = getenv("RBHIP_TILE_NT"))
-        if (w->dtype == RB_F64 && atoi(ev) == 256) w->tile_nt = 256;
-    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
-    int64_t nf = 0;
-    for (int64_t b = 0; b < w->N; ++b) {
-        const double x = qpos[7 * b], y = qpos[7 * b + 1];
-        if (!(fabs(x) < 1e9 && fabs(y) < 1e9)) continue;
-        lo[0] = std::min(lo[0], x); hi[0] = std::max(hi[0], x);
-        lo[1] = std::min(lo[1], y); hi[1] = std::max(hi[1], y);
-        ++nf;
-    }
-    if (!nf) { w->tile_ntx = 0; return RB_OK; }
-    const double band = w->tile_band > 0 ? w->tile_band : 10.0 * w->rmax;
-    const double ex = std::max(hi[0] - lo[0], 1e-9), ey = std::max(hi[1] - lo[1], 1e-9);
-    const int64_t owned = w->tile_owned > 0 ? w->tile_owned : (w->dtype == RB_F64 ? 160 : 256);
-    double T = sqrt(ex * ey * (double)owned / (double)w->N);
-    T = std::max(T, std::max(2.5 * band, 8.0 * w->rmax));
-    // a tile's band must fit the workgroup's lanes: the fullest tile's
-    // density over (T + 2W)^2, with room to grow, within 90 % of them
-    const double floorT = std::max(2.5 * band, 8.0 * w->rmax);
-    T = std::max(T, floorT);
-    int64_t ntx = 0, nty = 0;
-    int32_t most = 0;
-    std::vector<int32_t> hist;
-    for (int attempt = 0;; ++attempt) {
-        for (;; T *= 1.1) {
-            ntx = std::max<int64_t>(1, (int64_t)ceil(ex / T));
-            nty = std::max<int64_t>(1, (int64_t)ceil(ey / T));
-            if (ntx * nty <= 65535) break;
-        }
-        hist.assign((size_t)(ntx * nty), 0);
-        most = 0;
-        for (int64_t b = 0; b < w->N; ++b) {
-            const double x = qpos[7 * b], y = qpos[7 * b + 1];
-            int64_t tx = (int64_t)((x - lo[0]) / T), ty = (int64_t)((y - lo[1]) / T);
-            tx = tx < 0 ? 0 : tx >= ntx ? ntx - 1 : tx;
-            ty = ty < 0 ? 0 : ty >= nty ? nty - 1 : ty;
-            most = std::max(most, ++hist[(size_t)(ty * ntx + tx)]);
-        }
-        const double loaded = (double)most / (T * T) * (T + 2 * band) * (T + 2 * band) * w->tile_room;
-        if (loaded <= 0.9 * w->tile_nt) break;
-        if (T <= floorT * 1.0001 || attempt > 40) { w->tile_ntx = 0; return RB_OK; }   // too dense to tile
-        T = std::max(floorT, T * 0.9);
-    }
-    int64_t cap = std::max<int64_t>(512, (2 * (int64_t)most + 63) / 64 * 64);
-    if (w->tile_cap_grow) cap = std::max<int64_t>(cap, 2 * (int64_t)w->tile_cap);
-    w->tile_cap_grow = false;
-    const int64_t ntile = ntx * nty;
-    if (ntile * cap != (int64_t)w->tile_ntx * w->tile_nty * w->tile_cap || !w->tile_rec) {
-        void *old[] = {w->tile_rec, w->tile_count};
-        for (void *b : old)
-            if (b) HIPCHK(hipFree(b));
-        w->tile_rec = nullptr; w->tile_count = nullptr;
-        const size_t rec = w->dtype == RB_F64 ? sizeof(TileRec<double>) : sizeof(TileRec<float>);
-        HIPCHK(hipMalloc(&w->tile_rec, rec * 2 * ntile * cap));
-        HIPCHK(hipMalloc((void **)&w->tile_count, sizeof(int32_t) * 2 * ntile));
-    }
-    if (!w->tile_ctl) HIPCHK(hipMalloc((void **)&w->tile_ctl, sizeof(TileCtl)));
-    if (!w->tile_ctl_host) HIPCHK(hipHostMalloc((void **)&w->tile_ctl_host, 2 * sizeof(TileCtl), 0));
-    w->tile_ntx = (int32_t)ntx;
-    w->tile_nty = (int32_t)nty;
-    w->tile_cap = (int32_t)cap;
-    w->tile_ox = lo[0];
-    w->tile_oy = lo[1];
-    w->tile_size = T;
-    return RB_OK;
-}
-
 int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     if (!w || !qpos || !qvel) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
@@ -1919,7 +1664,6 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     par_copy(w->io_q_h, qpos, nq);
     par_copy(w->io_v_h, qvel, nv);
     fit_period(w, qpos);
-    if (int rc = fit_tiles(w, qpos)) return rc;
     w->xb_cut_valid = false;                             // block slabs: refitted at the next block run
     HIPCHK(hipMemcpyAsync(w->io_q_d, w->io_q_h, sizeof(double) * nq, hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(w->io_v_d, w->io_v_h, sizeof(double) * nv, hipMemcpyHostToDevice, w->stream));
@@ -2335,39 +2079,17 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
 
 }  // extern "C"
 
-namespace {
-// refit the tile grid to the positions of the current step (the snapshot)
-int tile_refit(rb_world *w) {
-    std::vector<double> q((size_t)7 * w->N, 0.0);
-    const size_t n = (size_t)4 * w->Npad;
-    HIPCHK(hipStreamSynchronize(w->stream));
-    if (w->dtype == RB_F64) {
-        std::vector<double> s(n);
-        HIPCHK(hipMemcpy(s.data(), w->snap[w->sp()], sizeof(double) * n, hipMemcpyDeviceToHost));
-        for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = s[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = s[(size_t)(4 * b + 1)]; }
-    } else {
-        std::vector<float> s(n);
-        HIPCHK(hipMemcpy(s.data(), w->snap[w->sp()], sizeof(float) * n, hipMemcpyDeviceToHost));
-        for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = s[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = s[(size_t)(4 * b + 1)]; }
-    }
-    return fit_tiles(w, q.data());
-}
-}  // namespace
-
 extern "C" {
 
+// The LDS tile blocks of round 3 were retired in round 4: the
+// XCD-resident blocks (rb_xblock.hip) replace them.  The entry stays for ABI
+// compatibility: mode -1 / 0 are accepted (nothing to configure), 1 fails.
 int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned) {
     if (!w) return fail(RB_EINVAL, "null world");
     if (mode < -1 || mode > 1 || kmax < 0 || kmax > 64 || !(band >= 0) || owned < 0)
         return fail(RB_EINVAL, "bad tile configuration");
-    HIPCHK(hipSetDevice(w->device));
-    if (int rc = finish_pending(w)) return rc;
-    w->tile_mode = mode;
-    if (kmax) w->tile_kmax = kmax;
-    if (band > 0) w->tile_band = band;
-    if (owned) w->tile_owned = std::max<int64_t>(16, owned);
-    if (mode == 0 || w->P != 1 || !w->all_spheres) return RB_OK;
-    return tile_refit(w);
+    if (mode == 1) return fail(RB_EUNSUPPORTED, "the LDS tile blocks were retired; the XCD-resident blocks replace them");
+    return RB_OK;
 }
 
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
@@ -2375,10 +2097,7 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     const int form = step_form(w);
-    const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), w->tile_stats[0], w->tile_stats[1], w->tile_stats[2],
-                                       w->tile_stats[3], w->tile_stats[4], w->tile_stats[5], w->tile_stats[6],
-                                       form, (int64_t)w->tile_ntx * w->tile_nty, w->tile_nt, w->tile_kmax, w->tile_cap,
-                                       (int64_t)(w->tile_size * 1e6), tile_eligible(w, 1 << 20) ? 1 : 0,
+    const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), 0, 0, 0, 0, 0, 0, 0, form, 0, 0, 0, 0, 0, 0,
                                        w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H,
                                        (int64_t)w->maxp, w->xb_stats[0], w->xb_stats[1], w->xb_stats[2], w->xb_stats[3],
                                        (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0, w->io_stats[0], w->io_stats[1]};

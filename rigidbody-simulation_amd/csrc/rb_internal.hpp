@@ -256,73 +256,6 @@ template <typename T> struct HaloParams {
     T *quat;
 };
 
-// ---- K-step tile blocks (rb_tile.hip) ------------------------
-// The scene's xy extent is cut into square tiles (columns, z unbounded).  One
-// workgroup per tile loads its tile's bodies, a ghost band of width W around
-// them and an outer ring, builds each body's neighbour list once, and steps
-// the tile plus band K times in LDS and registers with one barrier per step.
-// A ghost is "tainted" once its state may differ from the true one (its
-// neighbours outside the loaded set are unknown); taint spreads only where a
-// tainted body's displacement bound reaches an untainted body.  The block is
-// exact iff no owned body is tainted and no owned body left its displacement
-// bound; otherwise the block is redone from the same start, shorter.
-// Bodies are stored per tile ("bins"), in the tile that owned them at the
-// last block start; bins ping-pong with the block parity.
-constexpr int TILE_MAXL = 16;          // neighbour-list entries per body
-constexpr int TILE_NCOL = 1024;        // LDS columns of the list build
-constexpr int32_t ERR_TILE = 1 << 20;  // tile capacity / band exhausted (host falls back; never user-visible)
-
-struct TileCtl {
-    // the run (host-initialised)
-    int64_t done, target;              // steps committed, steps requested
-    int32_t phase;                     // bins[phase] hold the committed state
-    int32_t k_s;                       // displacement-bound horizon of the block in flight
-    int32_t k_run;                     // steps of the block in flight (0: every later block is a no-op)
-    int32_t k_plan;                    // horizon of the next fresh block
-    uint32_t sig_max;                  // float bits: max speed bound over every body (committed state)
-    int32_t err;                       // ERR_TILE: the run stopped at `done`
-    int32_t blocks, redo_taint, redo_disp, restart;   // statistics
-    // accumulators of the block in flight (reset by its last workgroup)
-    int32_t acc_valid;                 // min over workgroups of the steps known exact
-    int32_t acc_err;
-    uint32_t acc_sig;                  // max over owned bodies of the new speed bound
-    uint32_t acc_done;                 // workgroups finished
-    int32_t acc_disp;                  // a displacement bound was left (statistics)
-    int32_t streak;                    // clean blocks in a row at the current horizon
-};
-
-// One body in a tile bin (array of structures: a lane moves its body with
-// 16-byte accesses; the bin pass reads x, y with one)
-template <typename T> struct alignas(16) TileRec {
-    T x, y, z, qw, qx, qy, qz, vx, vy, vz, wx, wy, wz;   // state
-    T m, ix, iy, iz, r;                                // constants (mass, principal inertia, radius)
-    int32_t id;                                        // global id
-    float sig;                                         // top speed over the owner's last block
-};
-
-template <typename T> struct TileParams {
-    TileRec<T> *rec;                   // [2][ntile][cap] body records, per tile
-    int32_t *count;                    // [2][ntile]
-    TileCtl *ctl;
-    int32_t ntile, ntx, nty, cap;
-    T ox, oy, tile, band;              // grid origin, tile edge, ghost band width W
-    T rmax;                            // largest radius in the scene
-    BodyConsts<T> cs;
-    int32_t n_planes;
-    T pn[MAX_PLANES][3], pp[MAX_PLANES][3];
-    T g[3];
-    T dt, e, mu, thr;
-    int32_t oriented, kmax;
-    int32_t *err;
-    // gather / scatter (canonical state <-> bins)
-    T *st_base;
-    int64_t S;
-    int32_t lo, n_local;
-    const Snap<T> *snap_in;            // gather: the step's snapshot
-    Snap<T> *snap_out[2];              // scatter: the snapshots by step parity
-    int64_t c0;                        // step counter at the start of the run
-};
-
 // ---- XCD-resident K-step blocks (rb_xblock.hip) -----------------
 // One launch steps the scene K times.  Its workgroups form XB_GROUPS groups
 // (blocks b, b + 8, b + 16, ... : the workgroups of one XCD, checked against
@@ -379,11 +312,6 @@ template <typename T> struct XbParams {
     int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) a wait may take
 };
 template <typename T> hipError_t launch_xblock(const XbParams<T> &p, int maxp, hipStream_t s);
-
-// launchers (rb_tile.hip)
-template <typename T> hipError_t launch_tile_gather(const TileParams<T> &p, hipStream_t s);
-template <typename T> hipError_t launch_tile_block(const TileParams<T> &p, int nt, hipStream_t s);
-template <typename T> hipError_t launch_tile_scatter(const TileParams<T> &p, hipStream_t s);
 
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one

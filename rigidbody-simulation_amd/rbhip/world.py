@@ -218,8 +218,9 @@ class World:
         return cnt, par[:t], kin[:t], dis[:t]
 
     def tile_config(self, mode: int = -1, kmax: int = 0, band: float = 0.0, owned: int = 0):
-        """K-step tile blocks (rb_tile_config): mode -1 auto, 0 off, 1 on;
-        kmax / band (m) / owned bodies per tile, 0 = keep."""
+        """Retired (rb_tile_config): mode -1 / 0 are accepted,
+        1 raises RB_EUNSUPPORTED; the XCD-resident K-step blocks replace the
+        tile blocks (stats()["xb_*"])."""
         _lib.check(self._L.rb_tile_config(self._h, int(mode), int(kmax), float(band), int(owned)), "rb_tile_config")
 
     def stats(self) -> dict:
