@@ -202,7 +202,8 @@ struct rb_world {
     void *xb_lsnap = nullptr, *xb_lstate = nullptr, *xb_lconst = nullptr;
     uint32_t *xb_lines = nullptr;  // [XB_GROUPS][2][H][32] the groups' bucket tables
     uint32_t *xb_spill = nullptr;  // [XB_GROUPS][2][2 + 2 SPILL_CAP]
-    int64_t xb_H = 0;              // buckets of those tables
+    int64_t xb_H = 0;              // buckets of those tables (their own linear layout, xb_group)
+    int32_t xb_group = 0;          // Grid::super of the block tables (8 x 8 x 4 cell groups, 4 heads per line)
     XbCtl *xb_ctl = nullptr;
     bool xb_pending = false;       // a run awaits its check (xb_finish)
     int64_t xb_c0 = 0, xb_n = 0;
@@ -726,8 +727,6 @@ bool xb_eligible(const rb_world *w, int64_t nsteps) {
     if (w->xb_mode == 0 || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
         return false;
     if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;   // (N <= 16,384 x wpg)
-    const int form = step_form(w);
-    if (form != FORM_WIDE && form != FORM_WIDE_HELP) return false;   // the block runs the wide form's body code
     if (nsteps < 2) return false;
     return w->xb_mode == 1 || w->N >= w->xb_min_bodies;
 }
@@ -756,6 +755,32 @@ void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride) {
         const double below = *std::max_element(u.begin(), u.begin() + k);
         w->xb_cut[g] = 0.5 * (below + u[k]);
     }
+    // the block tables' layout: groups of 8 x 8 x 4 cells laid out linearly
+    // (rb_grid.hpp bucket_linear), the period split over the axes so it
+    // covers the scene's extent as evenly as the table's size allows
+    const int gb[3] = {3, 3, 2};
+    double need[3];
+    for (int d = 0; d < 3; ++d) {
+        double l = 1e300, h = -1e300;
+        for (int64_t b = 0; b < w->N; ++b) { l = std::min(l, qpos[stride * b + d]); h = std::max(h, qpos[stride * b + d]); }
+        need[d] = (floor(h * w->inv_cs) - floor(l * w->inv_cs) + 3) / double(1 << gb[d]);
+    }
+    int lg = 0;
+    while ((int64_t(1) << (lg + 1)) <= w->xb_H) ++lg;
+    lg -= gb[0] + gb[1] + gb[2];
+    int l[3] = {0, 0, 0};
+    for (int k = 0; k < lg; ++k) {
+        int best = 0;
+        double bv = -1;
+        for (int d = 0; d < 3; ++d) {
+            const double v = need[d] / double(1 << l[d]);
+            if (l[d] < 15 && v > bv) { bv = v; best = d; }
+        }
+        ++l[best];
+    }
+    const int32_t grp = 0x233 | (l[0] << 12) | (l[1] << 16) | (l[2] << 20) | (1 << 24) | (2 << 25);
+    if (grp != w->xb_group) w->xb_sp_host.clear();       // (the step parameters carry the grid)
+    w->xb_group = grp;
     w->xb_cut_valid = true;
 }
 
@@ -776,8 +801,9 @@ int xb_refit_cuts(rb_world *w) {
     double old[XB_GROUPS + 1];
     memcpy(old, w->xb_cut, sizeof old);
     const int old_axis = w->xb_axis;
+    const int32_t old_group = w->xb_group;
     xb_fit_cuts(w, q.data(), 7);
-    if (memcmp(old, w->xb_cut, sizeof old) != 0 || old_axis != w->xb_axis)
+    if (memcmp(old, w->xb_cut, sizeof old) != 0 || old_axis != w->xb_axis || old_group != w->xb_group)
         drop_graphs(w);                                  // the cuts are captured kernel arguments
     return RB_OK;
 }
@@ -785,7 +811,7 @@ int xb_refit_cuts(rb_world *w) {
 // the groups' buffers (lazily, at the first eligible run; the tables again
 // when the world's table size changes)
 int xb_alloc(rb_world *w) {
-    if (w->xb_ctl && w->xb_H == w->H) return RB_OK;
+    if (w->xb_ctl) return RB_OK;
     HIPCHK(hipStreamSynchronize(w->stream));
     drop_graphs(w);
     if (!w->xb_ctl) {
@@ -811,17 +837,18 @@ int xb_alloc(rb_world *w) {
         HIPCHK(hipMemset(w->xb_ctl, 0, sizeof(XbCtl)));
         const size_t spb = (w->dtype == RB_F64 ? sizeof(StepParams<double>) : sizeof(StepParams<float>)) * XB_GROUPS * 4;
         HIPCHK(hipMalloc(&w->xb_sp, spb));
+        // 32 buckets per local body (as the wide form's tables), 2^14 .. 2^22
+        w->xb_H = std::min<int64_t>(std::max<int64_t>(next_pow2(32 * cap), int64_t(1) << 14), int64_t(1) << 22);
     }
     // the tables: generation-tagged like the world's (nothing is cleared), so
     // a fresh allocation is zeroed and every group starts at generation 2
     if (w->xb_lines) { HIPCHK(hipFree(w->xb_lines)); w->xb_lines = nullptr; }
-    const size_t words = (size_t)XB_GROUPS * 2 * LINE_WORDS * (size_t)w->H;
+    const size_t words = (size_t)XB_GROUPS * 2 * LINE_WORDS * (size_t)w->xb_H;
     HIPCHK(hipMalloc((void **)&w->xb_lines, sizeof(uint32_t) * words));
     HIPCHK(hipMemset(w->xb_lines, 0, sizeof(uint32_t) * words));
     HIPCHK(hipMemset(w->xb_spill, 0, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
     std::vector<uint32_t> gen((size_t)XB_GROUPS * 32, 2u);
     HIPCHK(hipMemcpy(w->xb_ctl->gen, gen.data(), sizeof(uint32_t) * gen.size(), hipMemcpyHostToDevice));
-    w->xb_H = w->H;
     w->xb_sp_host.clear();
     return RB_OK;
 }
@@ -845,8 +872,11 @@ template <typename T> int xb_upload_params(rb_world *w, double dt, double e, dou
             p.n_global = cap;
             p.S = (int32_t)cap;
             p.xfrc = nullptr;
+            p.grid.hmask = (uint32_t)(w->xb_H - 1);
+            p.grid.H = (int32_t)w->xb_H;
+            p.grid.super = w->xb_group;
             auto tab = [&](int q) {
-                return Table<T>{w->xb_lines + ((size_t)(2 * g + q) * LINE_WORDS * (size_t)w->H), nullptr, nullptr,
+                return Table<T>{w->xb_lines + ((size_t)(2 * g + q) * LINE_WORDS * (size_t)w->xb_H), nullptr, nullptr,
                                 w->xb_spill + (size_t)(2 * g + q) * (2 + 2 * SPILL_CAP)};
             };
             p.cur = tab(par);

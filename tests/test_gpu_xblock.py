@@ -127,3 +127,15 @@ def test_blocks_f32_bit_exact_vs_per_step(rb, monkeypatch):
     (q1, v1, st), (q0, v0, _) = _run_pair(rb, sc, monkeypatch, [40], k=8, dtype="f32")
     assert st["xb_steps"] == 40, st
     assert np.array_equal(q1, q0) and np.array_equal(v1, v0)
+
+
+@pytest.mark.parametrize("shape", ["c2", "slab8k"])
+def test_blocks_on_cooperative_form_worlds(rb, monkeypatch, shape):
+    """Worlds small enough for the cooperative per-step form (C2: 4,096
+    spheres; one rank's 256 x 32 slab of C3 at 8 GPUs: 8,192) step in blocks
+    on the blocks' own table layout: bit-identical to the per-step kernels."""
+    from rbhip import scenes
+    sc = scenes.make("c2") if shape == "c2" else scenes.flat_spheres(256, 32, seed=0)
+    (q1, v1, st), (q0, v0, _) = _run_pair(rb, sc, monkeypatch, [45, 30], k=6)
+    assert st["xb_steps"] == 75 and st["xb_fallbacks"] == 0, st
+    assert _same(q1, q0) and _same(v1, v0)
