@@ -111,7 +111,7 @@ void xblock_kernel(XbParams<T> P) {
     __shared__ uint32_t s_cand[WIDE_MAXC * XB_THREADS];
     __shared__ uint8_t s_didx[1];
     __shared__ int s_w[XB_THREADS / 64];
-    __shared__ unsigned long long s_flag[XB_CHUNK / 64];   // the chunk's ids in the copy (one bit each)
+    __shared__ unsigned long long s_flag[XB_CHUNK / 64 + 32];   // the chunk's ids in the copy (one bit each)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = (int)(blockIdx.x % XB_GROUPS), r = (int)(blockIdx.x / XB_GROUPS), wpg = P.wpg;
     XbCtl *C = P.ctl;
@@ -125,10 +125,18 @@ void xblock_kernel(XbParams<T> P) {
     const int chunk = (P.n + wpg - 1) / wpg;
     const int c0 = r * chunk, c1 = min(P.n, c0 + chunk);
     float vm = 0.f;
-    for (int id = c0 + tid; id < c1; id += XB_THREADS) {
-        const T vx = P.st_base[4 * P.S + id], vy = P.st_base[5 * P.S + id], vz = P.st_base[6 * P.S + id];
-        const float v = (float)sqroot(vx * vx + vy * vy + vz * vz);
-        vm = (v > vm || v != v) ? v : vm;           // a NaN poisons the bound (the check then fails)
+    for (int b0 = c0; b0 < c1; b0 += 4 * XB_THREADS) {
+        T vv[4][3];                                  // four bodies' loads in flight together
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int id = min(b0 + q * XB_THREADS + tid, c1 - 1);
+            vv[q][0] = P.st_base[4 * P.S + id]; vv[q][1] = P.st_base[5 * P.S + id]; vv[q][2] = P.st_base[6 * P.S + id];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float v = (float)sqroot(vv[q][0] * vv[q][0] + vv[q][1] * vv[q][1] + vv[q][2] * vv[q][2]);
+            vm = (v > vm || v != v) ? v : vm;       // a NaN poisons the bound (the check then fails)
+        }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) { const float o = __shfl_xor(vm, off); vm = (o > vm || o != o) ? o : vm; }
@@ -161,17 +169,25 @@ void xblock_kernel(XbParams<T> P) {
     // ---- 2. the copy: this chunk's bodies within [lo, hi), flagged in LDS
     // (one bit per id of the chunk) and counted
     int cnt = 0;
-    for (int b0 = c0; b0 < c1; b0 += XB_THREADS) {
-        const int id = b0 + tid;
-        bool in = false;
-        if (id < c1) {
-            const T u = axis_of(P.snap_in[id], P.axis);
-            if (!(u == u)) atomicOr(P.err, ERR_DOMAIN);
-            in = u >= lo && u < hi;
+    for (int b0 = c0; b0 < c1; b0 += 4 * XB_THREADS) {
+        T u[4];                                      // four independent loads, then the flags
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int id = b0 + q * XB_THREADS + tid;
+            u[q] = id < c1 ? axis_of(P.snap_in[id], P.axis) : T(0);
         }
-        const unsigned long long m = __ballot(in);
-        if (lane == 0) s_flag[(b0 - c0) / 64 + wave] = m;
-        cnt += in ? 1 : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int id = b0 + q * XB_THREADS + tid;
+            bool in = false;
+            if (id < c1) {
+                if (!(u[q] == u[q])) atomicOr(P.err, ERR_DOMAIN);
+                in = u[q] >= lo && u[q] < hi;
+            }
+            const unsigned long long m = __ballot(in);
+            if (lane == 0) s_flag[(b0 + q * XB_THREADS - c0) / 64 + wave] = m;
+            cnt += in ? 1 : 0;
+        }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
