@@ -21,6 +21,9 @@ for step in "$@"; do
     case $step in
         xbtest) run xb_tests 600 python -u -m pytest tests/test_gpu_xblock.py -x -v --timeout 300 --timeout-method thread ;;
         xbtime) run xb_time 300 python -u scripts/xb_time.py --ks 0,2,4,6,8,12 ;;
+        xbtime8k) run xb_time_slab8k 300 python -u scripts/xb_time.py --config slab8k --ks 0,2,4,6,8,12,16 ;;
+        xbtimec2) run xb_time_c2 300 python -u scripts/xb_time.py --config c2 --ks 0,2,4,6,8,12,16 ;;
+        xbtimec4) run xb_time_c4 300 python -u scripts/xb_time.py --config c4 --start 260 --ks 0,4,8 ;;
         shims) run shims 300 python -u -m pytest tests/test_gpu_shims.py tests/test_gpu_threads.py -x -q --timeout 300 --timeout-method thread ;;
         c4ab) LIBS="rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline SIZES=256x256 WARM=500 \
               ENVS="RBHIP_XB=0" ROUNDS=2 run c4_pipe_ab 300 python -u scripts/ablate.py ;;

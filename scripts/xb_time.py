@@ -29,7 +29,8 @@ def main():
     import rbhip
     from rbhip import scenes
     rbhip.load()
-    sc = scenes.make(a.config)
+    # slab8k: one rank's 256 x 32 slab of C3 at 8 GPUs (8,192 bodies)
+    sc = scenes.flat_spheres(256, 32, seed=0) if a.config == "slab8k" else scenes.make(a.config)
     rows, ref = [], None
     for k in [int(x) for x in a.ks.split(",")]:
         os.environ["RBHIP_XB"] = "1" if k > 0 else "0"
