@@ -38,6 +38,8 @@
 // (rb_capi.hip xb_finish).  V = valpha max|v| + vbeta + K |g| dt, max|v| taken
 // over every body at the launch's start (each group scans all of them).
 #define RB_XB 1
+#undef RB_STAMPS
+#define RB_STAMPS 0              // (diagnostic stamp builds: the buffer lives in rb_kernels.hip's own unit)
 #define RB_STEP_BLOCK 512        // (rb_internal.hpp XB_THREADS): the wide form's LDS columns
 #define RB_WIDE_LDSPOS 0         // partner snapshots re-read in the solve (L2-resident here)
 #define RB_WIDE_QBATCH 8         // candidates per round trip: two waves per SIMD must fit in 256 registers
