@@ -21,12 +21,15 @@ Scaling (body-id range shards, positions exchanged every step):
                     8 GPUs" on one 65,536-sphere scene; N = 1 is the BENCH line.
   weak              N patches of the config side by side on one shared
                     ground, one per rank (per-GPU work fixed).
-The ranks exchange positions inside the library every step, peer-to-peer
-over xGMI, in one of two modes: halo pushes (each rank pushes to each peer
-only its bodies within a cell of the peer's bounds) or full slice reads.
-Both are warmed up, validated and timed over 20 steps on the node itself;
-the faster one runs the timed region (`config.exchange_probe_ms_per_step`
-lists both).  RCCL is the fallback when neither validates.
+The ranks exchange positions inside the library, peer-to-peer over xGMI,
+in one of three modes: halo pushes (each step, each rank pushes to each
+peer only its bodies within a cell of the peer's bounds), full slice reads
+(each step), or sharded K-step blocks (every K steps each rank pushes the
+full state of its bodies within the blocks' ghost band of each peer, then
+steps own bodies plus ghosts K times in XCD-resident blocks).  All are
+warmed up, validated and timed over 20 steps on the node itself; the
+fastest valid one runs the timed region (`config.exchange_probe_ms_per_step`
+lists them).  RCCL is the fallback when none validates.
 
 N > 1 is validated: after the warmup and again after the timed region, every
 rank's bodies must be bit-identical (compared as uint64 words, so the sign
@@ -43,8 +46,10 @@ roofline: algorithmic HBM bytes of the step kernel (248 B per
 sphere body-step in fp64) x owned bodies / its average launch duration.
 One rank: HIP events recorded on the world's stream (torch's current
 stream) around the timed region, which is exactly K graph-replayed
-step-kernel launches, / K.  Several ranks: an event pair around each
-step-kernel launch over a second run of K steps.  `traffic` /
+step-kernel launches, / K (with K-step blocks: the region's time / K, the
+blocks' launches).  Several ranks: an event pair around each step-kernel
+launch over a second run of K steps (sharded blocks: the region's time / K,
+pushes included).  `traffic` /
 `traffic_lower`: the PMC bounds per launch from the committed
 profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 command, profiles/collect_pmc.py), named in `traffic_source`;
@@ -359,12 +364,22 @@ def main():
     else:
         cands, probes = [], {}
         # last resort: torch.distributed's all-gather per step (host-driven)
-        for tr, halo in (("p2p", True), ("p2p", False), ("rccl", "auto"), ("nccl", False)):
+        for tr, halo, blocks in (("p2p", True, False), ("p2p", False, False), ("p2p", False, True),
+                                 ("rccl", "auto", False), ("nccl", False, False)):
             if tr in ("rccl", "nccl") and cands:
                 break
-            c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo,
-                             **WORLD_KW.get(args.config, {}))
-            name = c.transport + (" halo" if c.halo else " full reads" if c.transport == "p2p" else "")
+            try:
+                c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo, blocks=blocks,
+                                 **WORLD_KW.get(args.config, {}))
+            except Exception as ex:      # (the blocks need a sphere world's mailbox)
+                if rank == 0:
+                    print(f"bench: {tr} {'blocks ' if blocks else ''}unavailable: {ex}", file=sys.stderr, flush=True)
+                continue
+            if blocks and not c.blocks:
+                c.world.close()
+                continue
+            name = c.transport + (" blocks" if c.blocks else " halo" if c.halo else
+                                  " full reads" if c.transport == "p2p" else "")
             c.step(args.warmup)
             if not check(c, args.warmup):
                 if rank == 0:
@@ -421,7 +436,7 @@ def main():
     # region is exactly K back-to-back step-kernel launches (graph replay),
     # so HIP events around it / K.  Several ranks: a step also runs the
     # exchange, so time each step-kernel launch with its own event pair.
-    if P == 1 and blocked:
+    if blocked:
         # one launch steps K reference steps: the timed region is exactly the
         # run's block launches, so its HIP-event time / K steps is the time
         # per step (rocprofv3's per-launch average / K agrees)
@@ -458,7 +473,10 @@ def main():
         "timed_steps": timed,
         "config": {"workload": desc, "bodies_total": scene.n, "bodies_per_gpu": w.n_owned,
                    "parallelism": f"body-range shards x{P}" + (
-                       f", {sw.transport}{' halo' if sw.halo else ''} position exchange, graph-replayed" if P > 1 else ""),
+                       (f", {sw.transport} ghost pushes every {w.stats()['xb_k']} steps, XCD-resident blocks, "
+                        "graph-replayed" if sw.blocks else
+                        f", {sw.transport}{' halo' if sw.halo else ''} position exchange, graph-replayed")
+                       if P > 1 else ""),
                    "timed_steps": timed,
                    "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction,
                    **({"validated": f"bit-identical (uint64 words) to one World of the whole scene after "

@@ -215,6 +215,19 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len);
  * rb_p2p_connect and before stepping.  enable = 0 returns to full reads. */
 int rb_p2p_halo(rb_world *w, int32_t enable);
 
+/* Sharded K-step blocks (every rank alike, after rb_p2p_connect):
+ * mode 1 steps rb_shard_run calls of >= 2 steps (sphere worlds, the MuJoCo
+ * law, no applied forces, <= 16 partners) K steps per launch — each rank
+ * pushes to each peer the full state of its bodies within the blocks' ghost
+ * band of that peer's bodies, then steps its own bodies plus the ghosts K
+ * times in XCD-resident blocks (rb_xblock.hip).  Bit-exact with the
+ * per-step exchange; a run whose speed bound fails anywhere rolls back on
+ * every rank and replays per step.  0: per-step exchange (default).
+ * RB_EUNSUPPORTED: box worlds, or a mailbox made with RBHIP_XS=0.
+ * Replaces, for sharded runs, the per-step loop of multi_sphere_bounce.py:42-92
+ * like rb_shard_run. */
+int rb_shard_blocks(rb_world *w, int32_t mode);
+
 /* ---- the two-ball law -------------------------------------------------- */
 /* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
  * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;

@@ -211,6 +211,17 @@ struct rb_world {
     int64_t xb_stats[4] = {};      // runs, launches, steps committed, runs rolled back and replayed per step
     int32_t xb_backoff = 0;        // eligible runs to skip after a roll-back (doubles)
     int32_t xb_skip = 0;
+    bool xb_sharded = false;       // the pending run is a sharded one (XS)
+    // sharded K-step blocks (XS: rb_p2p.hip xs_push_kernel + the blocks'
+    // sharded form): peer-to-peer worlds, every rank alike
+    int xs_mode = 0;               // rb_shard_blocks: 0 off, 1 on
+    bool xs_mail = false;          // the mailbox lays out the XS regions (sphere worlds, RBHIP_XS != 0)
+    unsigned long long *xs_gidx = nullptr;   // [XB_GROUPS][Npad]
+    float *xs_part = nullptr;      // [push blocks][8]
+    unsigned long long *xs_done = nullptr;   // [2]
+    int32_t *xs_push_cnt = nullptr, *xs_in_cnt = nullptr;   // [P], [P]
+    int64_t *xs_epoch = nullptr;
+    void *xs_vw = nullptr;         // [2] T: the launch's V, W
     // the boundary's staging (rb_set_state / rb_get_state): pinned host rows
     // in the caller's layout and their device twins, moved with one DMA each
     // way and transposed by a kernel.  The staging mirrors the device state
@@ -464,7 +475,7 @@ template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
     hp.push_cnt = w->push_cnt;
     hp.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
     hp.mail = reinterpret_cast<const char *>(w->flags);
-    hp.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
+    hp.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
     hp.epoch = w->epoch;
     hp.rank = (int32_t)w->rank;
     hp.P = (int32_t)w->P;
@@ -732,39 +743,40 @@ bool xb_eligible(const rb_world *w, int64_t nsteps) {
 }
 
 // the slabs: equal body counts along the widest horizontal axis (x, y) of
-// the positions qpos (stride 7); group g owns [cut[g], cut[g+1])
-void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride) {
-    w->xb_cut_valid = false;
-    if (w->N < XB_GROUPS) return;
-    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
-    for (int64_t b = 0; b < w->N; ++b)
-        for (int d = 0; d < 2; ++d) {
+// the n positions qpos (stride 7); group g owns [cut[g], cut[g+1]).  Fewer
+// than XB_GROUPS bodies, or a non-finite position: group 0 owns everything
+// (the block launch then reports the position; a shard's choice must not
+// differ from its peers', so the blocks still run)
+void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride, int64_t n) {
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    bool finite = true;
+    for (int64_t b = 0; b < n; ++b)
+        for (int d = 0; d < 3; ++d) {
             const double u = qpos[stride * b + d];
-            if (!(u == u) || fabs(u) > 1e12) return;     // (non-finite: the per-step kernels report it)
+            if (!(u == u) || fabs(u) > 1e12) { finite = false; continue; }
             lo[d] = std::min(lo[d], u);
             hi[d] = std::max(hi[d], u);
         }
-    w->xb_axis = (hi[1] - lo[1]) > (hi[0] - lo[0]) ? 1 : 0;
-    std::vector<double> u((size_t)w->N);
-    for (int64_t b = 0; b < w->N; ++b) u[(size_t)b] = qpos[stride * b + w->xb_axis];
     w->xb_cut[0] = -INFINITY;
-    w->xb_cut[XB_GROUPS] = INFINITY;
-    for (int g = 1; g < XB_GROUPS; ++g) {
-        const size_t k = (size_t)((int64_t)w->N * g / XB_GROUPS);
-        std::nth_element(u.begin(), u.begin() + k, u.end());
-        const double below = *std::max_element(u.begin(), u.begin() + k);
-        w->xb_cut[g] = 0.5 * (below + u[k]);
+    for (int g = 1; g <= XB_GROUPS; ++g) w->xb_cut[g] = INFINITY;
+    w->xb_axis = (hi[1] - lo[1]) > (hi[0] - lo[0]) ? 1 : 0;
+    if (finite && n >= XB_GROUPS) {
+        std::vector<double> u((size_t)n);
+        for (int64_t b = 0; b < n; ++b) u[(size_t)b] = qpos[stride * b + w->xb_axis];
+        for (int g = 1; g < XB_GROUPS; ++g) {
+            const size_t k = (size_t)(n * g / XB_GROUPS);
+            std::nth_element(u.begin(), u.begin() + k, u.end());
+            const double below = *std::max_element(u.begin(), u.begin() + k);
+            w->xb_cut[g] = 0.5 * (below + u[k]);
+        }
     }
     // the block tables' layout: groups of 8 x 8 x 4 cells laid out linearly
     // (rb_grid.hpp bucket_linear), the period split over the axes so it
     // covers the scene's extent as evenly as the table's size allows
     const int gb[3] = {3, 3, 2};
     double need[3];
-    for (int d = 0; d < 3; ++d) {
-        double l = 1e300, h = -1e300;
-        for (int64_t b = 0; b < w->N; ++b) { l = std::min(l, qpos[stride * b + d]); h = std::max(h, qpos[stride * b + d]); }
-        need[d] = (floor(h * w->inv_cs) - floor(l * w->inv_cs) + 3) / double(1 << gb[d]);
-    }
+    for (int d = 0; d < 3; ++d)
+        need[d] = hi[d] >= lo[d] ? (floor(hi[d] * w->inv_cs) - floor(lo[d] * w->inv_cs) + 3) / double(1 << gb[d]) : 1.0;
     int lg = 0;
     while ((int64_t(1) << (lg + 1)) <= w->xb_H) ++lg;
     lg -= gb[0] + gb[1] + gb[2];
@@ -784,25 +796,27 @@ void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride) {
     w->xb_cut_valid = true;
 }
 
-// the slabs fitted to the positions of the current step (the snapshot)
+// the slabs fitted to the positions of the current step (the snapshot; a
+// shard: its own bodies)
 int xb_refit_cuts(rb_world *w) {
-    std::vector<double> q((size_t)7 * w->N, 0.0);
-    const size_t ne = (size_t)4 * w->N;
+    const int64_t n = w->n_local, lo = w->lo;
+    std::vector<double> q((size_t)7 * (n > 0 ? n : 1), 0.0);
+    const size_t ne = (size_t)4 * n;
     HIPCHK(hipStreamSynchronize(w->stream));
     if (w->dtype == RB_F64) {
         std::vector<double> sn(ne);
-        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sizeof(double) * ne, hipMemcpyDeviceToHost));
-        for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; }
+        HIPCHK(hipMemcpy(sn.data(), dp<double>(w->snap[w->sp()], 4 * lo), sizeof(double) * ne, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < n; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; q[(size_t)(7 * b + 2)] = sn[(size_t)(4 * b + 2)]; }
     } else {
         std::vector<float> sn(ne);
-        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sizeof(float) * ne, hipMemcpyDeviceToHost));
-        for (int64_t b = 0; b < w->N; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; }
+        HIPCHK(hipMemcpy(sn.data(), dp<float>(w->snap[w->sp()], 4 * lo), sizeof(float) * ne, hipMemcpyDeviceToHost));
+        for (int64_t b = 0; b < n; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; q[(size_t)(7 * b + 2)] = sn[(size_t)(4 * b + 2)]; }
     }
     double old[XB_GROUPS + 1];
     memcpy(old, w->xb_cut, sizeof old);
     const int old_axis = w->xb_axis;
     const int32_t old_group = w->xb_group;
-    xb_fit_cuts(w, q.data(), 7);
+    xb_fit_cuts(w, q.data(), 7, n);
     if (memcmp(old, w->xb_cut, sizeof old) != 0 || old_axis != w->xb_axis || old_group != w->xb_group)
         drop_graphs(w);                                  // the cuts are captured kernel arguments
     return RB_OK;
@@ -819,10 +833,18 @@ int xb_alloc(rb_world *w) {
         int cus = 0;
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, w->device));
         w->xb_wpg = (cus % XB_GROUPS == 0 && cus / XB_GROUPS >= 1 && cus / XB_GROUPS <= XB_MAX_WPG) ? cus / XB_GROUPS : 0;
+        // RBHIP_XB_WPG=n (tests): n workgroups per group, so that the launches
+        // of ranks sharing one GPU fit on it together (2 x 16 per XCD)
+        if (const char *ev = getenv("RBHIP_XB_WPG")) {
+            const int v = atoi(ev);
+            if (w->xb_wpg && v >= 1 && v <= w->xb_wpg) w->xb_wpg = v;
+        }
         if (!w->xb_wpg) return RB_OK;
         // room for the slab and a band of up to half its width on each side
         // (a wider copy fails the block: the chunk replays step by step)
-        int64_t cap = std::min<int64_t>(w->N, 2 * ((w->N + XB_GROUPS - 1) / XB_GROUPS) + 8192);
+        // (a shard: its own bodies' slab plus own and pushed ghosts)
+        const int64_t own = w->P > 1 ? w->n_local : w->N;
+        int64_t cap = std::min<int64_t>(w->N, 2 * ((own + XB_GROUPS - 1) / XB_GROUPS) + 8192);
         cap = (cap + 63) / 64 * 64;
         w->xb_cap = (int32_t)cap;
         const size_t esz = (size_t)w->esz;
@@ -926,6 +948,48 @@ template <typename T> XbParams<T> make_xb(rb_world *w, int64_t c, int K, double 
     p.ctl = w->xb_ctl;
     p.err = w->err;
     p.timeout_ticks = 50000000;        // 0.5 s at 100 MHz
+    if (w->P > 1) {                    // sharded (XS): own rows at id - lo, ghosts from the mailbox
+        p.xs = 1;
+        p.lo = (int32_t)w->lo;
+        p.n_local = (int32_t)w->n_local;
+        p.P = (int32_t)w->P;
+        p.mail = reinterpret_cast<const char *>(w->flags);
+        p.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
+        p.in_cnt = w->xs_in_cnt;
+        p.vw = static_cast<const T *>(w->xs_vw);
+        p.xs_epoch = w->xs_epoch;
+        p.gidx = w->xs_gidx;
+        p.Npad = w->Npad;
+    }
+    return p;
+}
+
+template <typename T> XsPushParams<T> make_xs_push(rb_world *w, int64_t c, int K, double dt) {
+    XsPushParams<T> p{};
+    p.snap = dp<Snap<T>>(w->snap[c % 2], 0);
+    p.st = BodyState<T>{dp<T>(w->state, 0), w->S};
+    p.lo = (int32_t)w->lo;
+    p.n_local = (int32_t)w->n_local;
+    p.rank = (int32_t)w->rank;
+    p.P = (int32_t)w->P;
+    p.S = w->S;
+    p.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
+    p.mail = reinterpret_cast<char *>(w->flags);
+    p.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
+    p.part = w->xs_part;
+    p.done = w->xs_done;
+    p.push_cnt = w->xs_push_cnt;
+    p.xs_epoch = w->xs_epoch;
+    p.vw = static_cast<T *>(w->xs_vw);
+    p.in_cnt = w->xs_in_cnt;
+    p.K = K;
+    p.reach = (T)(2.0 * w->rmax);
+    p.gdt = (T)(sqrt(w->g[0] * w->g[0] + w->g[1] * w->g[1] + w->g[2] * w->g[2]) * dt);
+    p.dt = (T)dt;
+    p.valpha = (T)w->xb_valpha;
+    p.vbeta = (T)w->xb_vbeta;
+    p.err = w->err;
+    p.timeout_ticks = 500000000;       // 5 s at 100 MHz (as the per-step exchange)
     return p;
 }
 
@@ -941,23 +1005,65 @@ int xb_enqueue(rb_world *w, hipStream_t s, int64_t c0, int64_t n, double dt) {
     return RB_OK;
 }
 
+// Sharded (XS): per block of K steps, the push kernel (headers, ghosts,
+// counts: rb_p2p.hip) and the block launch; after the run's last block a
+// final push (headers and counts only: every rank learns whether any rank
+// failed, and that every peer's last block committed) and the gather of
+// every peer's snapshot slice, so the per-step path finds the whole scene.
+int xs_enqueue(rb_world *w, hipStream_t s, int64_t c0, int64_t n, double dt) {
+    const bool f64 = w->dtype == RB_F64;
+    for (int64_t done = 0; done < n;) {
+        const int K = (int)std::min<int64_t>(w->xb_k, n - done);
+        HIPCHK(f64 ? launch_xs_push<double>(make_xs_push<double>(w, c0 + done, K, dt), s)
+                   : launch_xs_push<float>(make_xs_push<float>(w, c0 + done, K, dt), s));
+        HIPCHK(f64 ? launch_xblock<double>(make_xb<double>(w, c0 + done, K, dt), w->maxp, s)
+                   : launch_xblock<float>(make_xb<float>(w, c0 + done, K, dt), w->maxp, s));
+        done += K;
+    }
+    const int64_t ce = c0 + n;
+    HIPCHK(f64 ? launch_xs_push<double>(make_xs_push<double>(w, ce, 0, dt), s)
+               : launch_xs_push<float>(make_xs_push<float>(w, ce, 0, dt), s));
+    const int sp = (int)(ce % 2);
+    if (f64)
+        HIPCHK(launch_xs_gather<double>(dp<Snap<double>>(w->snap[sp], 0),
+                                        reinterpret_cast<const Snap<double> *const *>(w->peer_snap_dev + sp * w->P),
+                                        (int32_t)w->rank, (int32_t)w->P, w->S, w->N, s));
+    else
+        HIPCHK(launch_xs_gather<float>(dp<Snap<float>>(w->snap[sp], 0),
+                                       reinterpret_cast<const Snap<float> *const *>(w->peer_snap_dev + sp * w->P),
+                                       (int32_t)w->rank, (int32_t)w->P, w->S, w->N, s));
+    return RB_OK;
+}
+
+bool xs_eligible(const rb_world *w, int64_t nsteps) {
+    if (w->xs_mode != 1 || w->P < 2 || !w->p2p || !w->xs_mail || !w->all_spheres || w->law != RB_LAW_MUJOCO ||
+        w->xfrc || w->timing)
+        return false;
+    if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;
+    return nsteps >= 2;
+}
+
 // A run of n steps in blocks: the chunk-start state is saved (the blocks
 // commit in place), the launches replay from a graph, and the run is checked
 // at the next sync point (xb_finish; at once for a synchronous rb_step).
 int xb_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
+    const bool sh = w->P > 1;                // sharded (XS): every rank runs the same launches
     if (int rc = xb_alloc(w)) return rc;
     if (!w->xb_cut_valid)
         if (int rc = xb_refit_cuts(w)) return rc;
-    if (!w->xb_wpg || !w->xb_cut_valid) {
-        if (!w->xb_wpg) w->xb_mode = 0;      // the device cannot run the blocks
-        return enqueue_steps(w, n, dt, e, mu, thr, false, false);
+    if (!w->xb_wpg) {
+        w->xb_mode = 0;                      // the device cannot run the blocks
+        w->xs_mode = 0;
+        return enqueue_steps(w, n, dt, e, mu, thr, sh, false);
     }
     int rc = w->dtype == RB_F64 ? xb_upload_params<double>(w, dt, e, mu, thr) : xb_upload_params<float>(w, dt, e, mu, thr);
     if (rc) return rc;
     if ((rc = chunk_save(w))) return rc;
-    rc = graph_replay(w, n, 8, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) { return xb_enqueue(w, s, c0, n, dt); });
+    rc = sh ? graph_replay(w, n, 9, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) { return xs_enqueue(w, s, c0, n, dt); })
+            : graph_replay(w, n, 8, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) { return xb_enqueue(w, s, c0, n, dt); });
     if (rc) return rc;
     w->xb_pending = true;
+    w->xb_sharded = sh;
     w->xb_c0 = w->c;
     w->xb_n = n;
     w->xb_prm[0] = dt; w->xb_prm[1] = e; w->xb_prm[2] = mu; w->xb_prm[3] = thr;
@@ -993,14 +1099,17 @@ int xb_finish(rb_world *w) {
     // generations stay: they only grow)
     HIPCHK(hipMemset(w->xb_ctl, 0, offsetof(XbCtl, cnt)));
     HIPCHK(hipMemset(&w->xb_ctl->poison, 0, 2 * sizeof(int32_t)));
-    if (ctl.why & (XB_WHY_PLACEMENT | XB_WHY_TIMEOUT)) w->xb_mode = 0;
+    // (a shard: every rank rolled back alike — the push kernels spread an
+    // error to every rank — and must keep deciding alike, so only the
+    // back-off, which every rank advances the same way, applies)
+    if (!w->xb_sharded && (ctl.why & (XB_WHY_PLACEMENT | XB_WHY_TIMEOUT))) w->xb_mode = 0;
     w->xb_backoff = w->xb_backoff ? std::min(2 * w->xb_backoff, 64) : 1;
     w->xb_skip = w->xb_backoff;
     w->c = w->xb_c0;
     if (int rc = chunk_restore(w)) return rc;
     if (ctl.why & XB_WHY_CAP) w->xb_cut_valid = false;   // the slabs drifted: refit at the next run
     const double *q = w->xb_prm;
-    return enqueue_steps(w, w->xb_n, q[0], q[1], q[2], q[3], false, false);
+    return enqueue_steps(w, w->xb_n, q[0], q[1], q[2], q[3], w->xb_sharded, false);
 }
 
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
@@ -1016,7 +1125,8 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     w->state_version += 1;
-    if (!sharded && allow_xb && xb_eligible(w, w->record ? nsteps - 1 : nsteps)) {
+    if (allow_xb && (sharded ? xs_eligible(w, w->record ? nsteps - 1 : nsteps)
+                             : xb_eligible(w, w->record ? nsteps - 1 : nsteps))) {
         if (w->xb_skip > 0) {
             --w->xb_skip;                        // (back-off after a roll-back: this run steps per step)
         } else {
@@ -1288,7 +1398,8 @@ void free_world(rb_world *w) {
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     void *tbufs[] = {w->opt_save, w->xb_sp, w->xb_map, w->xb_lkind, w->xb_lsnap,
-                     w->xb_lstate, w->xb_lconst, w->xb_lines, w->xb_spill, w->xb_ctl};
+                     w->xb_lstate, w->xb_lconst, w->xb_lines, w->xb_spill, w->xb_ctl,
+                     w->xs_gidx, w->xs_part, w->xs_done, w->xs_push_cnt, w->xs_in_cnt, w->xs_epoch, w->xs_vw};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->defer_host) (void)hipHostFree(w->defer_host);
@@ -1853,8 +1964,11 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
     HIPCHK(hipSetDevice(w->device));
     if (!w->flags) {
         // the mailbox, uncached: peers write it over xGMI while this rank's
-        // kernels poll and read it
-        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
+        // kernels poll and read it.  Sphere worlds lay out the sharded
+        // blocks' regions too (RBHIP_XS=0: not; every rank must agree)
+        const char *xe = getenv("RBHIP_XS");
+        w->xs_mail = !w->boxes && !(xe && atoi(xe) == 0) && w->P <= 64;
+        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
         HIPCHK(hipExtMallocWithFlags((void **)&w->flags, (size_t)lay.bytes, hipDeviceMallocUncached));
         HIPCHK(hipMemset(w->flags, 0, (size_t)lay.bytes));
     }
@@ -1918,6 +2032,38 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     HIPCHK(hipDeviceSynchronize());
     w->p2p = true;
     drop_graphs(w);
+    return RB_OK;
+}
+
+// Sharded K-step blocks (XS): every rank of a peer-to-peer world
+// alike.  The buffers are made at the first enable.
+int rb_shard_blocks(rb_world *w, int32_t mode) {
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (mode != 0 && mode != 1) return fail(RB_EINVAL, "mode must be 0 or 1");
+    HIPCHK(hipSetDevice(w->device));
+    if (int rc = finish_pending(w)) return rc;
+    if (mode == 1) {
+        if (!w->p2p) return fail(RB_EINVAL, "rb_shard_blocks before rb_p2p_connect");
+        if (!w->xs_mail) return fail(RB_EUNSUPPORTED, "sharded blocks: sphere worlds whose mailbox lays them out (RBHIP_XS != 0)");
+        if (!w->xs_gidx) {
+            HIPCHK(hipStreamSynchronize(w->stream));
+            const int64_t nb = std::max<int64_t>(1, (w->n_local + XS_PUSH_BLOCK - 1) / XS_PUSH_BLOCK);
+            HIPCHK(hipMalloc((void **)&w->xs_gidx, sizeof(unsigned long long) * XB_GROUPS * w->Npad));
+            HIPCHK(hipMemset(w->xs_gidx, 0, sizeof(unsigned long long) * XB_GROUPS * w->Npad));
+            HIPCHK(hipMalloc((void **)&w->xs_part, sizeof(float) * 8 * nb));
+            HIPCHK(hipMalloc((void **)&w->xs_done, sizeof(unsigned long long) * 2));
+            HIPCHK(hipMemset(w->xs_done, 0, sizeof(unsigned long long) * 2));
+            HIPCHK(hipMalloc((void **)&w->xs_push_cnt, sizeof(int32_t) * w->P));
+            HIPCHK(hipMemset(w->xs_push_cnt, 0, sizeof(int32_t) * w->P));
+            HIPCHK(hipMalloc((void **)&w->xs_in_cnt, sizeof(int32_t) * w->P));
+            HIPCHK(hipMemset(w->xs_in_cnt, 0, sizeof(int32_t) * w->P));
+            HIPCHK(hipMalloc((void **)&w->xs_epoch, sizeof(int64_t)));
+            HIPCHK(hipMemset(w->xs_epoch, 0, sizeof(int64_t)));
+            HIPCHK(hipMalloc(&w->xs_vw, 2 * sizeof(double)));
+        }
+    }
+    if (w->xs_mode != mode) drop_graphs(w);
+    w->xs_mode = mode;
     return RB_OK;
 }
 

@@ -106,7 +106,14 @@ __device__ __forceinline__ int block_scan(int f, int *s_w, int *tot) {
 template <typename T>
 __device__ __forceinline__ T axis_of(const Snap<T> &s, int axis) { return axis == 0 ? s.x : s.y; }
 
-template <typename T, int MAXP>
+// sharded worlds: the mailbox's pushed rows (written by the peers over
+// xGMI into this rank's uncached mailbox), read past the caches
+template <typename T> __device__ __forceinline__ T ld_sys(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long ld_sc1_ull(const unsigned long long *p) { return ld_sc1(p); }
+
+template <typename T, int MAXP, bool SH>
 __global__ __launch_bounds__(XB_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void xblock_kernel(XbParams<T> P) {
     __shared__ int32_t s_id[MAXP * XB_THREADS];
@@ -122,32 +129,63 @@ void xblock_kernel(XbParams<T> P) {
     const int cap = P.cap;
     if (tid == 0) __hip_atomic_store(&C->xcc[blockIdx.x], xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-    // ---- 1. every group scans every body: max |v| (the launch's speed
-    // bound), each workgroup a contiguous id chunk
+    // ---- 1. the launch's speed bound V and band W.  One rank: every group
+    // scans every body for max |v|, each workgroup a contiguous id chunk.
+    // Sharded (SH): the push kernel made them from every rank's header; the
+    // group instead indexes the ghosts the peers pushed (gidx: id -> inbox
+    // slot, tagged with the push's epoch)
     const int chunk = (P.n + wpg - 1) / wpg;
     const int c0 = r * chunk, c1 = min(P.n, c0 + chunk);
-    float vm = 0.f;
-    for (int b0 = c0; b0 < c1; b0 += 4 * XB_THREADS) {
-        T vv[4][3];                                  // four bodies' loads in flight together
+    T V, W;
+    float vmax = 0.f;
+    [[maybe_unused]] int64_t e = 0, G = 0;
+    [[maybe_unused]] const uint32_t *in_ids = nullptr;
+    [[maybe_unused]] const T *in_pay = nullptr;
+    [[maybe_unused]] unsigned long long *gx = nullptr;
+    if constexpr (SH) {
+        e = *P.xs_epoch;
+        G = P.lay.xg;
+        const int par = (int)(e & 1);
+        in_ids = reinterpret_cast<const uint32_t *>(P.mail + P.lay.o_xids) + (int64_t)par * P.P * G;
+        in_pay = reinterpret_cast<const T *>(P.mail + P.lay.o_xpay) + (int64_t)par * P.P * XS_PAY * G;
+        gx = P.gidx + (int64_t)g * P.Npad;
+        int tot = 0;
+        for (int q = 0; q < P.P; ++q) tot += P.in_cnt[q];
+        for (int k = r * XB_THREADS + tid; k < tot; k += wpg * XB_THREADS) {
+            int q = 0, o = k;
+            while (o >= P.in_cnt[q]) { o -= P.in_cnt[q]; ++q; }
+            const uint32_t id = ld_sys(in_ids + (int64_t)q * G + o);
+            if ((int64_t)id < (int64_t)q * P.S || (int64_t)id >= (int64_t)(q + 1) * P.S || (int64_t)id >= P.n) {
+                atomicOr(P.err, ERR_XB);
+                continue;
+            }
+            gx[id] = ((unsigned long long)e << 32) | (unsigned long long)(q * G + o);
+        }
+        V = P.vw[0];
+        W = P.vw[1];
+    } else {
+        for (int b0 = c0; b0 < c1; b0 += 4 * XB_THREADS) {
+            T vv[4][3];                                  // four bodies' loads in flight together
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int id = min(b0 + q * XB_THREADS + tid, c1 - 1);
-            vv[q][0] = P.st_base[4 * P.S + id]; vv[q][1] = P.st_base[5 * P.S + id]; vv[q][2] = P.st_base[6 * P.S + id];
+            for (int q = 0; q < 4; ++q) {
+                const int id = min(b0 + q * XB_THREADS + tid, c1 - 1);
+                vv[q][0] = P.st_base[4 * P.S + id]; vv[q][1] = P.st_base[5 * P.S + id]; vv[q][2] = P.st_base[6 * P.S + id];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float v = (float)sqroot(vv[q][0] * vv[q][0] + vv[q][1] * vv[q][1] + vv[q][2] * vv[q][2]);
+                vmax = (v > vmax || v != v) ? v : vmax;       // a NaN poisons the bound (the check then fails)
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float v = (float)sqroot(vv[q][0] * vv[q][0] + vv[q][1] * vv[q][1] + vv[q][2] * vv[q][2]);
-            vm = (v > vm || v != v) ? v : vm;       // a NaN poisons the bound (the check then fails)
+        for (int off = 32; off >= 1; off >>= 1) { const float o = __shfl_xor(vmax, off); vmax = (o > vmax || o != o) ? o : vmax; }
+        if (lane == 0) s_w[wave] = (int)__float_as_uint(vmax);
+        __syncthreads();
+        if (tid == 0) {
+            float m = 0.f;
+            for (int k = 0; k < XB_THREADS / 64; ++k) { const float o = __uint_as_float((uint32_t)s_w[k]); m = (o > m || o != o) ? o : m; }
+            C->vpart[g][r] = __float_as_uint(m);
         }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) { const float o = __shfl_xor(vm, off); vm = (o > vm || o != o) ? o : vm; }
-    if (lane == 0) s_w[wave] = (int)__float_as_uint(vm);
-    __syncthreads();
-    if (tid == 0) {
-        float m = 0.f;
-        for (int k = 0; k < XB_THREADS / 64; ++k) { const float o = __uint_as_float((uint32_t)s_w[k]); m = (o > m || o != o) ? o : m; }
-        C->vpart[g][r] = __float_as_uint(m);
     }
     xb_barrier(C, g, wpg, t0, tmo, P.err);
     // the placement check: every workgroup of the group on one XCD
@@ -156,33 +194,60 @@ void xblock_kernel(XbParams<T> P) {
         atomicOr(&C->why, XB_WHY_PLACEMENT);
         atomicOr(P.err, ERR_XB);
     }
-    float vmax = 0.f;
-    for (int k = 0; k < wpg; ++k) {
-        const float o = __uint_as_float(__hip_atomic_load(&C->vpart[g][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        vmax = (o > vmax || o != o) ? o : vmax;
+    if constexpr (!SH) {
+        vmax = 0.f;
+        for (int k = 0; k < wpg; ++k) {
+            const float o = __uint_as_float(__hip_atomic_load(&C->vpart[g][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            vmax = (o > vmax || o != o) ? o : vmax;
+        }
+        V = P.valpha * (T)vmax + P.vbeta + (T)P.K * P.gdt;
+        W = (T)P.K * P.reach + T(2) * (T)(P.K - 1) * V * P.sp[0].dt + T(1e-3) * P.reach;
+        if (g == 0 && r == 0 && tid == 0) C->vmax_bits = __float_as_uint(vmax);
     }
-    const T V = P.valpha * (T)vmax + P.vbeta + (T)P.K * P.gdt;
     const T V2 = V * V;
-    const T W = (T)P.K * P.reach + T(2) * (T)(P.K - 1) * V * P.sp[0].dt + T(1e-3) * P.reach;
     const T lo = g == 0 ? -INFINITY : P.cut[g] - W, hi = g == XB_GROUPS - 1 ? INFINITY : P.cut[g + 1] + W;
     const T olo = g == 0 ? -INFINITY : P.cut[g], ohi = g == XB_GROUPS - 1 ? INFINITY : P.cut[g + 1];
-    if (g == 0 && r == 0 && tid == 0) C->vmax_bits = __float_as_uint(vmax);
+    // sharded: where body id's step-start position comes from (own rows, a
+    // ghost's inbox slot, or absent: -1)
+    [[maybe_unused]] auto ghost_slot = [&](int id) -> int64_t {
+        const unsigned long long t = xld(gx + id);
+        return (int64_t)(t >> 32) == e ? (int64_t)(uint32_t)t : -1;
+    };
+    [[maybe_unused]] auto own = [&](int id) { return id >= P.lo && id < P.lo + P.n_local; };
 
     // ---- 2. the copy: this chunk's bodies within [lo, hi), flagged in LDS
     // (one bit per id of the chunk) and counted
     int cnt = 0;
     for (int b0 = c0; b0 < c1; b0 += 4 * XB_THREADS) {
         T u[4];                                      // four independent loads, then the flags
+        [[maybe_unused]] bool have[4] = {true, true, true, true};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int id = b0 + q * XB_THREADS + tid;
-            u[q] = id < c1 ? axis_of(P.snap_in[id], P.axis) : T(0);
+            if constexpr (SH) {
+                u[q] = T(0);
+                have[q] = false;
+                if (id < c1) {
+                    if (own(id)) {
+                        u[q] = axis_of(P.snap_in[id], P.axis);
+                        have[q] = true;
+                    } else {
+                        const int64_t sl = ghost_slot(id);
+                        if (sl >= 0) {
+                            u[q] = ld_sys(in_pay + ((sl / G) * XS_PAY + P.axis) * G + sl % G);
+                            have[q] = true;
+                        }
+                    }
+                }
+            } else {
+                u[q] = id < c1 ? axis_of(P.snap_in[id], P.axis) : T(0);
+            }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int id = b0 + q * XB_THREADS + tid;
             bool in = false;
-            if (id < c1) {
+            if (id < c1 && have[q]) {
                 if (!(u[q] == u[q])) atomicOr(P.err, ERR_DOMAIN);
                 in = u[q] >= lo && u[q] < hi;
             }
@@ -240,12 +305,23 @@ void xblock_kernel(XbParams<T> P) {
         const int l = ((p * (XB_THREADS / 64) + wave) * wpg + r) * 64 + lane;
         if (l >= n) continue;
         const int id = xld(map + l);
-        const Snap<T> s = P.snap_in[id];
-        const T u = axis_of(s, P.axis);
-        if (u >= olo && u < ohi) owned |= 1u << p;
-        ls0[l] = s;
+        Snap<T> s;
+        if (!SH || own(id)) {
+            s = P.snap_in[id];
+            const int64_t row = SH ? id - P.lo : id;
 #pragma unroll
-        for (int k = 0; k < 13; ++k) lst[(int64_t)k * cap + l] = P.st_base[(int64_t)k * P.S + id];
+            for (int k = 0; k < 13; ++k) lst[(int64_t)k * cap + l] = P.st_base[(int64_t)k * P.S + row];
+            const T u = axis_of(s, P.axis);
+            if (u >= olo && u < ohi) owned |= 1u << p;
+        } else if constexpr (SH) {
+            int64_t sl = ghost_slot(id);             // (present: it was copied)
+            if (sl < 0) { atomicOr(P.err, ERR_XB); sl = 0; }
+            const T *src = in_pay + (sl / G) * XS_PAY * G + sl % G;
+            s.x = ld_sys(src); s.y = ld_sys(src + G); s.z = ld_sys(src + 2 * G); s.r = ld_sys(src + 3 * G);
+#pragma unroll
+            for (int k = 0; k < 13; ++k) lst[(int64_t)k * cap + l] = ld_sys(src + (4 + k) * G);
+        }
+        ls0[l] = s;
 #pragma unroll
         for (int k = 0; k < 8; ++k) lcs[(int64_t)k * cap + l] = P.cs.base[(int64_t)k * P.cs.Npad + id];
         lkd[l] = P.cs.kind[id];
@@ -304,8 +380,9 @@ void xblock_kernel(XbParams<T> P) {
         if (l >= n || !((owned >> p) & 1u)) continue;
         const int id = xld(map + l);
         P.snap_out[id] = lsK[l];                     // (written by this lane)
+        const int64_t row = SH ? id - P.lo : id;
 #pragma unroll
-        for (int k = 0; k < 13; ++k) P.st_base[(int64_t)k * P.S + id] = lst[(int64_t)k * cap + l];
+        for (int k = 0; k < 13; ++k) P.st_base[(int64_t)k * P.S + row] = lst[(int64_t)k * cap + l];
     }
     // the group's next table generation (read by the next launch only)
     if (r == 0 && tid == 0) C->gen[g][0] = gen0 + (uint32_t)P.K + 1u;
@@ -313,9 +390,14 @@ void xblock_kernel(XbParams<T> P) {
 
 template <typename T> hipError_t launch_xblock(const XbParams<T> &p, int maxp, hipStream_t s) {
     if (p.wpg < 1 || p.wpg > XB_MAX_WPG || p.K < 1 || !p.sp || !p.ctl) return hipErrorInvalidValue;
+    if (maxp > 16) return hipErrorInvalidValue;   // 32 partners: the LDS lists do not fit (per-step kernels)
     const dim3 grid((unsigned)(XB_GROUPS * p.wpg));
-    if (maxp <= 16) hipLaunchKernelGGL((xblock_kernel<T, 16>), grid, dim3(XB_THREADS), 0, s, p);
-    else return hipErrorInvalidValue;          // 32 partners: the LDS lists do not fit (per-step kernels)
+    if (p.xs) {
+        if (!p.mail || !p.in_cnt || !p.vw || !p.xs_epoch || !p.gidx || p.lay.o_xpay < 0 || p.P < 2) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((xblock_kernel<T, 16, true>), grid, dim3(XB_THREADS), 0, s, p);
+    } else {
+        hipLaunchKernelGGL((xblock_kernel<T, 16, false>), grid, dim3(XB_THREADS), 0, s, p);
+    }
     return hipGetLastError();
 }
 

@@ -192,6 +192,12 @@ class World:
         can reach); collective, after p2p_connect."""
         _lib.check(self._L.rb_p2p_halo(self._h, 1 if enable else 0), "rb_p2p_halo")
 
+    def shard_blocks(self, enable: bool = True):
+        """Sharded K-step blocks (rb_shard_blocks): shard_run calls step K
+        steps per launch with a ghost push per block; collective (every rank
+        alike), after p2p_connect."""
+        _lib.check(self._L.rb_shard_blocks(self._h, 1 if enable else 0), "rb_shard_blocks")
+
     def shard_run(self, nsteps: int = 1, dt=None, restitution=None, friction=None, threshold=None):
         """nsteps sharded steps with the in-library exchange (enqueued only)."""
         p = self._params(dt, restitution, friction, threshold)
