@@ -733,6 +733,95 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
     return RB_OK;
 }
 
+// The period-split scoring shared by fit_period (the world's tables) and
+// xb_fit_cuts (the blocks' tables): group keys packed 21 bits per axis.
+constexpr int64_t PERIOD_OFF = 1 << 20;                  // group coordinates kept in [-2^20, 2^20)
+inline int64_t period_pack(int64_t gx, int64_t gy, int64_t gz) {
+    return ((gx + PERIOD_OFF) << 42) | ((gy + PERIOD_OFF) << 21) | (gz + PERIOD_OFF);
+}
+inline int64_t period_unpack(int64_t k, int d) { return ((k >> (42 - 21 * d)) & ((1 << 21) - 1)) - PERIOD_OFF; }
+// The groups a search reads (the occupied ones, sorted unique, and their
+// neighbours; above 8,192 occupied groups the occupied ones alone), with
+// their coordinates and an occupied flag.
+struct PeriodSet {
+    std::vector<int64_t> qg[3];
+    std::vector<uint8_t> qocc;
+    explicit PeriodSet(std::vector<int64_t> occ) {
+        std::sort(occ.begin(), occ.end());
+        occ.erase(std::unique(occ.begin(), occ.end()), occ.end());
+        std::vector<int64_t> q;
+        q.reserve(occ.size() * 27);
+        if (occ.size() > 8192) q = occ;
+        else for (int64_t k : occ)
+            for (int dz = -1; dz <= 1; ++dz)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx)
+                        q.push_back(period_pack(period_unpack(k, 0) + dx, period_unpack(k, 1) + dy, period_unpack(k, 2) + dz));
+        std::sort(q.begin(), q.end());
+        q.erase(std::unique(q.begin(), q.end()), q.end());
+        qocc.resize(q.size());
+        for (int d = 0; d < 3; ++d) qg[d].resize(q.size());
+        for (size_t t = 0; t < q.size(); ++t) {
+            for (int d = 0; d < 3; ++d) qg[d][t] = period_unpack(q[t], d);
+            qocc[t] = std::binary_search(occ.begin(), occ.end(), q[t]) ? 1 : 0;
+        }
+    }
+    // groups a search reads that share a run of buckets with another group,
+    // at least one of them occupied, under the period 2^l[0] x 2^l[1] x 2^l[2]
+    int64_t collisions(const int l[3], std::vector<uint64_t> &f) const {
+        f.resize(qocc.size());
+        for (size_t t = 0; t < qocc.size(); ++t) {
+            uint64_t idx = 0;
+            int sh = 0;
+            for (int d = 0; d < 3; ++d) {
+                idx |= ((uint64_t)qg[d][t] & ((1ull << l[d]) - 1)) << sh;
+                sh += l[d];
+            }
+            f[t] = (idx << 1) | qocc[t];
+        }
+        std::sort(f.begin(), f.end());
+        int64_t coll = 0;
+        for (size_t a = 0; a < f.size();) {
+            size_t e = a;
+            bool any_occ = false;
+            while (e < f.size() && (f[e] >> 1) == (f[a] >> 1)) any_occ |= (f[e++] & 1);
+            if (any_occ) coll += (int64_t)(e - a) - 1;
+            a = e;
+        }
+        return coll;
+    }
+};
+// The split of lg period bits with the fewest collisions summed over the
+// sets; ties: fewest axes the period does not cover (need[d]: groups of
+// extent per axis), then the most even cover.
+inline void best_period_split(const std::vector<PeriodSet> &sets, const double need[3], int lg, int best[3]) {
+    std::vector<uint64_t> f;
+    int64_t best_c = -1;
+    int best_nf = 0;
+    double best_fold = 0.0;
+    for (int lx = 0; lx <= lg && lx <= 15; ++lx)
+        for (int ly = 0; lx + ly <= lg && ly <= 15; ++ly) {
+            const int lz = lg - lx - ly;
+            if (lz > 15) continue;
+            const int l[3] = {lx, ly, lz};
+            int64_t coll = 0;
+            for (const PeriodSet &ps : sets) coll += ps.collisions(l, f);
+            double fold = 0.0;
+            int nf = 0;                                  // axes the period does not cover
+            for (int d = 0; d < 3; ++d) {
+                fold = std::max(fold, need[d] / double(1 << l[d]));
+                nf += need[d] > double(1 << l[d]);
+            }
+            if (best_c < 0 || coll < best_c || (coll == best_c && nf < best_nf) ||
+                (coll == best_c && nf == best_nf && fold < best_fold - 1e-12)) {
+                best_c = coll;
+                best_nf = nf;
+                best_fold = fold;
+                best[0] = lx; best[1] = ly; best[2] = lz;
+            }
+        }
+}
+
 // ---- XCD-resident K-step blocks (rb_xblock.hip) ----------------
 bool xb_eligible(const rb_world *w, int64_t nsteps) {
     if (w->xb_mode == 0 || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
@@ -771,25 +860,40 @@ void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride, int64_t n) {
         }
     }
     // the block tables' layout: groups of 8 x 8 x 4 cells laid out linearly
-    // (rb_grid.hpp bucket_linear), the period split over the axes so it
-    // covers the scene's extent as evenly as the table's size allows
+    // (rb_grid.hpp bucket_linear), the period split scored like the world's
+    // (fit_period), by the collisions within each group's copy (its slab
+    // and an estimated band: a group's table holds only its copy)
     const int gb[3] = {3, 3, 2};
-    double need[3];
-    for (int d = 0; d < 3; ++d)
-        need[d] = hi[d] >= lo[d] ? (floor(hi[d] * w->inv_cs) - floor(lo[d] * w->inv_cs) + 3) / double(1 << gb[d]) : 1.0;
     int lg = 0;
     while ((int64_t(1) << (lg + 1)) <= w->xb_H) ++lg;
     lg -= gb[0] + gb[1] + gb[2];
-    int l[3] = {0, 0, 0};
-    for (int k = 0; k < lg; ++k) {
-        int best = 0;
-        double bv = -1;
-        for (int d = 0; d < 3; ++d) {
-            const double v = need[d] / double(1 << l[d]);
-            if (l[d] < 15 && v > bv) { bv = v; best = d; }
+    double need[3] = {1.0, 1.0, 1.0};
+    const double band = 1.5 * w->xb_k * 2.0 * w->rmax;
+    std::vector<std::vector<int64_t>> occ(XB_GROUPS);
+    for (int g = 0; g < XB_GROUPS; ++g) {
+        const double rlo = g == 0 ? -INFINITY : w->xb_cut[g] - band, rhi = g == XB_GROUPS - 1 ? INFINITY : w->xb_cut[g + 1] + band;
+        double glo[3] = {1e300, 1e300, 1e300}, ghi[3] = {-1e300, -1e300, -1e300};
+        for (int64_t b = 0; b < n; ++b) {
+            const double u = qpos[stride * b + w->xb_axis];
+            if (!(u >= rlo && u < rhi)) continue;
+            int64_t c[3];
+            bool ok = true;
+            for (int d = 0; d < 3; ++d) {
+                const double v = qpos[stride * b + d] * w->inv_cs;
+                if (!(v == v && v > -1e9 && v < 1e9)) { ok = false; break; }
+                glo[d] = std::min(glo[d], v);
+                ghi[d] = std::max(ghi[d], v);
+                c[d] = (int64_t)floor(v) >> gb[d];
+            }
+            if (ok) occ[(size_t)g].push_back(period_pack(c[0], c[1], c[2]));
         }
-        ++l[best];
+        for (int d = 0; d < 3; ++d)
+            if (ghi[d] >= glo[d]) need[d] = std::max(need[d], (floor(ghi[d]) - floor(glo[d]) + 2) / double(1 << gb[d]));
     }
+    std::vector<PeriodSet> sets;
+    for (auto &o : occ) sets.emplace_back(std::move(o));
+    int l[3] = {lg, 0, 0};
+    best_period_split(sets, need, lg, l);
     const int32_t grp = 0x233 | (l[0] << 12) | (l[1] << 16) | (l[2] << 20) | (1 << 24) | (2 << 25);
     if (grp != w->xb_group) w->xb_sp_host.clear();       // (the step parameters carry the grid)
     w->xb_group = grp;
@@ -1672,11 +1776,6 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
         if (atoi(ev) == 0) return;                       // diagnostic: keep the creation-time split
     const int gb[3] = {w->group & 15, (w->group >> 4) & 15, (w->group >> 8) & 15};
     const int lg = ((w->group >> 12) & 15) + ((w->group >> 16) & 15) + ((w->group >> 20) & 15);
-    constexpr int64_t OFF = 1 << 20;                     // group coordinates kept in [-2^20, 2^20)
-    auto pack = [](int64_t gx, int64_t gy, int64_t gz) {
-        return ((gx + OFF) << 42) | ((gy + OFF) << 21) | (gz + OFF);
-    };
-    auto unpack = [](int64_t k, int d) { return ((k >> (42 - 21 * d)) & ((1 << 21) - 1)) - OFF; };
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     std::vector<int64_t> occ;
     occ.reserve((size_t)w->N);
@@ -1689,9 +1788,9 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
             lo[d] = c < lo[d] ? c : lo[d];
             hi[d] = c > hi[d] ? c : hi[d];
             g[d] = (int64_t)floor(c) >> gb[d];
-            if (g[d] <= -OFF + 1 || g[d] >= OFF - 1) ok = false;
+            if (g[d] <= -PERIOD_OFF + 1 || g[d] >= PERIOD_OFF - 1) ok = false;
         }
-        if (ok) occ.push_back(pack(g[0], g[1], g[2]));
+        if (ok) occ.push_back(period_pack(g[0], g[1], g[2]));
     }
     // the split depends on the occupied groups; a call whose groups span
     // the same box as the last fit's (every frame of a per-frame caller:
@@ -1701,8 +1800,8 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
         int64_t gb_lo[3] = {INT64_MAX, INT64_MAX, INT64_MAX}, gb_hi[3] = {INT64_MIN, INT64_MIN, INT64_MIN};
         for (int64_t k : occ)
             for (int d = 0; d < 3; ++d) {
-                gb_lo[d] = std::min(gb_lo[d], unpack(k, d));
-                gb_hi[d] = std::max(gb_hi[d], unpack(k, d));
+                gb_lo[d] = std::min(gb_lo[d], period_unpack(k, d));
+                gb_hi[d] = std::max(gb_hi[d], period_unpack(k, d));
             }
         const int64_t key[7] = {gb_lo[0], gb_lo[1], gb_lo[2], gb_hi[0], gb_hi[1], gb_hi[2], (int64_t)w->group};
         const char *ev = getenv("RBHIP_FIT_PERIOD");
@@ -1710,74 +1809,13 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
         memcpy(w->fit_key, key, sizeof key);
         w->fit_valid = true;
     }
-    std::sort(occ.begin(), occ.end());
-    occ.erase(std::unique(occ.begin(), occ.end()), occ.end());
-    // the groups a search reads: the occupied ones and their neighbours
-    // (flag bit 0: occupied)
-    // (above 8,192 occupied groups the occupied ones alone: the split search
-    // stays well under a second at 4M bodies)
-    std::vector<int64_t> q;
-    q.reserve(occ.size() * 27);
-    if (occ.size() > 8192) q = occ;
-    else for (int64_t k : occ)
-        for (int dz = -1; dz <= 1; ++dz)
-            for (int dy = -1; dy <= 1; ++dy)
-                for (int dx = -1; dx <= 1; ++dx)
-                    q.push_back(pack(unpack(k, 0) + dx, unpack(k, 1) + dy, unpack(k, 2) + dz));
-    std::sort(q.begin(), q.end());
-    q.erase(std::unique(q.begin(), q.end()), q.end());
-    std::vector<int64_t> qg[3];
-    std::vector<uint8_t> qocc(q.size());
-    for (int d = 0; d < 3; ++d) qg[d].resize(q.size());
-    for (size_t t = 0; t < q.size(); ++t) {
-        for (int d = 0; d < 3; ++d) qg[d][t] = unpack(q[t], d);
-        qocc[t] = std::binary_search(occ.begin(), occ.end(), q[t]) ? 1 : 0;
-    }
     double need[3];
     for (int d = 0; d < 3; ++d)
         need[d] = hi[d] >= lo[d] ? (floor(hi[d]) - floor(lo[d]) + 2) / double(1 << gb[d]) : 1.0;
-    std::vector<uint64_t> f(q.size());
     int best[3] = {(w->group >> 12) & 15, (w->group >> 16) & 15, (w->group >> 20) & 15};
-    int64_t best_c = -1;
-    int best_nf = 0;
-    double best_fold = 0.0;
-    for (int lx = 0; lx <= lg && lx <= 15; ++lx)
-        for (int ly = 0; lx + ly <= lg && ly <= 15; ++ly) {
-            const int lz = lg - lx - ly;
-            if (lz > 15) continue;
-            const int l[3] = {lx, ly, lz};
-            for (size_t t = 0; t < q.size(); ++t) {
-                uint64_t idx = 0;
-                int sh = 0;
-                for (int d = 0; d < 3; ++d) {
-                    idx |= ((uint64_t)qg[d][t] & ((1ull << l[d]) - 1)) << sh;
-                    sh += l[d];
-                }
-                f[t] = (idx << 1) | qocc[t];
-            }
-            std::sort(f.begin(), f.end());
-            int64_t coll = 0;
-            for (size_t a = 0; a < f.size();) {
-                size_t e = a;
-                bool any_occ = false;
-                while (e < f.size() && (f[e] >> 1) == (f[a] >> 1)) any_occ |= (f[e++] & 1);
-                if (any_occ) coll += (int64_t)(e - a) - 1;
-                a = e;
-            }
-            double fold = 0.0;
-            int nf = 0;                                  // axes the period does not cover
-            for (int d = 0; d < 3; ++d) {
-                fold = std::max(fold, need[d] / double(1 << l[d]));
-                nf += need[d] > double(1 << l[d]);
-            }
-            if (best_c < 0 || coll < best_c || (coll == best_c && nf < best_nf) ||
-                (coll == best_c && nf == best_nf && fold < best_fold - 1e-12)) {
-                best_c = coll;
-                best_nf = nf;
-                best_fold = fold;
-                best[0] = lx; best[1] = ly; best[2] = lz;
-            }
-        }
+    std::vector<PeriodSet> sets;
+    sets.emplace_back(std::move(occ));
+    best_period_split(sets, need, lg, best);
     const int32_t g = (w->group & ~(0xfff << 12)) | (best[0] << 12) | (best[1] << 16) | (best[2] << 20);
     if (g != w->group) {
         w->group = g;
