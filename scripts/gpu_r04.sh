@@ -32,6 +32,10 @@ for step in "$@"; do
         framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
         pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ;;
+        benchK) run bench_k400 300 python -u bench.py --steps 400 --warmup 5 ;;
+        profdrv) run prof_driver 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_driver -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+        profk) run prof_k400 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_k400 -o run -- python bench.py --steps 400 --warmup 5 --no-cpu-baseline ;;
+        pmc) run pmc_c3 600 python -u profiles/collect_pmc.py c3 f64 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
