@@ -36,6 +36,9 @@ for step in "$@"; do
         profdrv) run prof_driver 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_driver -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
         profk) run prof_k400 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_k400 -o run -- python bench.py --steps 400 --warmup 5 --no-cpu-baseline ;;
         pmc) run pmc_c3 600 python -u profiles/collect_pmc.py c3 f64 ;;
+        c4win) run bench_c4_261 300 python -u bench.py --config c4 --warmup 60 --steps 200 --no-cpu-baseline &&
+               run bench_c4_451 300 python -u bench.py --config c4 --warmup 50 --steps 400 --no-cpu-baseline &&
+               run bench_c4_1801 600 python -u bench.py --config c4 --warmup 1600 --steps 200 --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -87,3 +87,43 @@ def test_band_matters(oracle):
     W = K * reach + 2 * (K - 1) * V * sc.dt + 1e-3 * reach
     bad, _ = _block_check(oracle, sc, q, v, K, shrink=W)
     assert bad > 0
+
+
+def test_sharded_copies_with_pushed_ghosts_are_exact(oracle):
+    """The sharded blocks' argument (rb_p2p.hip xs_push_kernel):
+    rank r owns ids [rS, rS + S); a peer pushes every body within W of r's
+    bounding box (x and y) — the ghosts; each of r's 8 groups copies its
+    slab of r's bodies plus every own body or ghost within W along the slab
+    axis.  Stepped K steps by the oracle, every rank's owned bodies match
+    the whole scene bit for bit (C3-like scene in 4 row slabs of 96 x 24)."""
+    sc = scenes.flat_spheres(96, 96, seed=0)
+    osc = oracle.OracleScene(sc)
+    q, v = oracle.step(osc, sc.qpos0, sc.qvel0, 25)
+    K, P = 6, 4
+    qk, vk = oracle.step(osc, q, v, K)
+    n = sc.n
+    S = -(-n // P)
+    reach = 2 * float(np.max(sc.size[:, 0]))
+    vmax = float(np.linalg.norm(v[:, :3], axis=1).max())
+    V = 1.5 * vmax + 0.5 + K * float(np.linalg.norm(sc.gravity)) * sc.dt
+    W = K * reach + 2 * (K - 1) * V * sc.dt + 1e-3 * reach
+    bad = 0
+    for r in range(P):
+        own = np.arange(r * S, min(n, r * S + S))
+        lo, hi = q[own, :2].min(0), q[own, :2].max(0)
+        others = np.setdiff1d(np.arange(n), own)
+        near = np.all((q[others, :2] >= lo - W) & (q[others, :2] <= hi + W), axis=1)
+        ghosts = others[near]
+        ext = hi - lo
+        axis = 1 if ext[1] > ext[0] else 0
+        u = np.sort(q[own, axis])
+        cut = [-np.inf] + [0.5 * (u[len(u) * g // G - 1] + u[len(u) * g // G]) for g in range(1, G)] + [np.inf]
+        pool = np.union1d(own, ghosts)
+        for g in range(G):
+            a, b = (cut[g] - W if g else -np.inf), (cut[g + 1] + W if g < G - 1 else np.inf)
+            ids = pool[(q[pool, axis] >= a) & (q[pool, axis] < b)]
+            mine = np.isin(ids, own) & (q[ids, axis] >= cut[g]) & (q[ids, axis] < cut[g + 1])
+            q1, v1 = oracle.step(oracle.OracleScene(_sub(sc, ids)), q[ids], v[ids], K)
+            bad += int((~(np.all(q1[mine].view(np.uint64) == qk[ids[mine]].view(np.uint64), axis=1) &
+                          np.all(v1[mine].view(np.uint64) == vk[ids[mine]].view(np.uint64), axis=1))).sum())
+    assert bad == 0
