@@ -644,41 +644,38 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
             }
         };
 #if RB_WIDE_PIPE
-        // Software-pipelined over the (bucket, slot batch) sequence: the ids
-        // of the next batch load under the current batch's snapshots, so a
-        // crowded neighbourhood (C4's pile-ups: 8 buckets of ~30 ids) costs
-        // one dependent round trip per batch instead of two
-        int k = 0, s0 = WIDE_HEAD_IDS - QB;
-        auto next_batch = [&]() -> bool {        // (k, s0) <- the next batch with ids left
-            s0 += QB;
-            while (k < 8) {
-                if (s0 < (int32_t)s_cand[(8 + k) * NB + tid]) return true;
-                ++k;
-                s0 = WIDE_HEAD_IDS;
-            }
-            return false;
-        };
+        // Software-pipelined, and batched across buckets: a batch takes the
+        // next QB ids past the heads of whichever buckets still have some
+        // (padding: the body itself, which never hits), and the ids of the
+        // next batch load under the current batch's snapshots — a crowded
+        // neighbourhood (C4's pile-ups: buckets of 7-30 ids) costs one
+        // dependent round trip per QB candidates, not one or two per bucket
+        int k = 0, s = WIDE_HEAD_IDS;
         uint32_t tjn[QB];
-        auto load_ids = [&]() {
-            const uint32_t bk = s_cand[k * NB + tid];
-            const int32_t ck = (int32_t)s_cand[(8 + k) * NB + tid];
+        auto load_ids = [&]() -> bool {           // the next batch's ids from cursor (k, s)
+            bool any = false;
 #pragma unroll
-            for (int u = 0; u < QB; ++u) tjn[u] = s0 + u < ck ? xld(slot_word(p.cur, bk, s0 + u, rl)) : (uint32_t)i;
+            for (int u = 0; u < QB; ++u) {
+                while (k < 8 && s >= (int32_t)s_cand[(8 + k) * NB + tid]) { ++k; s = WIDE_HEAD_IDS; }
+                tjn[u] = (uint32_t)i;
+                if (k < 8) {
+                    tjn[u] = xld(slot_word(p.cur, s_cand[k * NB + tid], s, rl));
+                    ++s;
+                    any = true;
+                }
+            }
+            return any;
         };
-        bool have = next_batch();
-        if (have) load_ids();
+        bool have = load_ids();
 #pragma unroll 1
         while (have) {
             uint32_t tj[QB];
 #pragma unroll
             for (int u = 0; u < QB; ++u) tj[u] = tjn[u];
-            const int scur = s0;
-            const int32_t ccur = (int32_t)s_cand[(8 + k) * NB + tid];
             Snap<T> sn[QB];
             gather(tj, sn);
-            have = next_batch();
-            if (have) load_ids();
-            test(tj, sn, scur, ccur);
+            have = load_ids();
+            test(tj, sn, 0, QB);
         }
 #else
 #pragma unroll 1
