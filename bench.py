@@ -262,7 +262,17 @@ class SingleWorldCheck:
         if self.rank == 0:
             import rbhip
             if self.ref is None:
-                self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype, **self.kw)
+                # the reference steps with the per-step kernels (RBHIP_XB=0),
+                # independent of the K-step blocks a mode under test may use
+                saved = os.environ.get("RBHIP_XB")
+                os.environ["RBHIP_XB"] = "0"
+                try:
+                    self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype, **self.kw)
+                finally:
+                    if saved is None:
+                        del os.environ["RBHIP_XB"]
+                    else:
+                        os.environ["RBHIP_XB"] = saved
             self.ref.step(steps_total - self.done)
             self.done = steps_total
             q1, v1 = self.ref.get_state()
