@@ -25,8 +25,8 @@ for step in "$@"; do
         xbtimec2) run xb_time_c2 300 python -u scripts/xb_time.py --config c2 --ks 0,2,4,6,8,12,16 ;;
         xbtimec4) run xb_time_c4 300 python -u scripts/xb_time.py --config c4 --start 260 --ks 0,4,8 ;;
         shims) run shims 300 python -u -m pytest tests/test_gpu_shims.py tests/test_gpu_threads.py -x -q --timeout 300 --timeout-method thread ;;
-        c4ab) LIBS="rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline SIZES=256x256 WARM=500 \
-              ENVS="RBHIP_XB=0" ROUNDS=2 run c4_pipe_ab 300 python -u scripts/ablate.py ;;
+        c4ab) run c4_pipe_ab 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline \
+              SIZES=256x256 WARM=500 ENVS=RBHIP_XB=0 ROUNDS=2 python -u scripts/ablate.py ;;
         xsmp) run xs_mp 600 python -u -m pytest tests/test_gpu_shard_mp.py -x -v -k "sharded_blocks or two_process_shards_match_single_world and p2p" --timeout 300 --timeout-method thread ;;
         stampsc4) run stamps_c4 300 python -u scripts/stamps_c4.py --warm 700 ;;
         framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
@@ -35,7 +35,7 @@ for step in "$@"; do
         benchK) run bench_k400 300 python -u bench.py --steps 400 --warmup 5 ;;
         profdrv) run prof_driver 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_driver -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
         profk) run prof_k400 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_k400 -o run -- python bench.py --steps 400 --warmup 5 --no-cpu-baseline ;;
-        rehxs) RBHIP_BENCH_BACKEND=gloo RBHIP_SHARD_TRANSPORT=p2p RBHIP_XB_WPG=16 run rehearse2_xs 600 \
+        rehxs) run rehearse2_xs 600 env RBHIP_BENCH_BACKEND=gloo RBHIP_SHARD_TRANSPORT=p2p RBHIP_XB_WPG=16 \
                    python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                    --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline ;;
         pmc) run pmc_c3 600 python -u profiles/collect_pmc.py c3 f64 ;;
