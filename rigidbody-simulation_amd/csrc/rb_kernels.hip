@@ -978,7 +978,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
     if (p.bounds) fold_bounds(p.bounds, cell);
 }
 
-#if RB_STAMPS && (!defined(RB_INST) || (RB_INST & 1))
+#if RB_STAMPS && (!defined(RB_INST) || (RB_INST & 1)) && (!defined(RB_WIDE_UNIT) || RB_WIDE_UNIT == 1)
 extern "C" int rb_diag_stamps(unsigned long long *out, int nblocks) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 16 * nblocks);
 }
