@@ -20,7 +20,7 @@ run() {   # name, seconds, command...
 for step in "$@"; do
     case $step in
         xbtest) run xb_tests 600 python -u -m pytest tests/test_gpu_xblock.py -x -v --timeout 300 --timeout-method thread ;;
-        xbtime) run xb_time 300 python -u scripts/xb_time.py --ks 0,2,4,6,8,12 ;;
+        xbtime) run xb_time 300 python -u scripts/xb_time.py --ks 0,2,4,6,8,12,16 ;;
         xbtime8k) run xb_time_slab8k 300 python -u scripts/xb_time.py --config slab8k --ks 0,2,4,6,8,12,16 ;;
         xbtimec2) run xb_time_c2 300 python -u scripts/xb_time.py --config c2 --ks 0,2,4,6,8,12,16 ;;
         xbtimec4) run xb_time_c4 300 python -u scripts/xb_time.py --config c4 --start 260 --ks 0,4,8 ;;
