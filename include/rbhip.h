@@ -228,6 +228,12 @@ int rb_p2p_halo(rb_world *w, int32_t enable);
  * like rb_shard_run. */
 int rb_shard_blocks(rb_world *w, int32_t mode);
 
+/* Diagnostic: the last K-step block launch's phase stamps (s_memrealtime,
+ * 100 MHz), 8 per workgroup — start, speed bound, counts, map, copy, step 0,
+ * last step, end — for n_wg workgroups (8 x wpg of them: workgroup b is
+ * group b % 8); *wpg receives the workgroups per group. */
+int rb_diag_xb_stamps(rb_world *w, uint64_t *out, int32_t n_wg, int32_t *wpg);
+
 /* ---- the two-ball law -------------------------------------------------- */
 /* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
  * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;

@@ -2073,6 +2073,18 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     return RB_OK;
 }
 
+// diagnostic: the last block launch's phase stamps, [workgroups][8]
+int rb_diag_xb_stamps(rb_world *w, uint64_t *out, int32_t n_wg, int32_t *wpg) {
+    if (!w || !out) return fail(RB_EINVAL, "null argument");
+    if (!w->xb_ctl) return fail(RB_EINVAL, "no block launch yet");
+    HIPCHK(hipSetDevice(w->device));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const int32_t nw = std::min<int32_t>(n_wg, XB_GROUPS * XB_MAX_WPG);
+    HIPCHK(hipMemcpy(out, w->xb_ctl->stamp, sizeof(uint64_t) * XB_STAMPS * nw, hipMemcpyDeviceToHost));
+    if (wpg) *wpg = w->xb_wpg;
+    return RB_OK;
+}
+
 // Sharded K-step blocks (XS): every rank of a peer-to-peer world
 // alike.  The buffers are made at the first enable.
 int rb_shard_blocks(rb_world *w, int32_t mode) {

@@ -296,6 +296,7 @@ template <typename T> struct HaloParams {
 constexpr int XB_GROUPS = 8;
 constexpr int XB_THREADS = 512;        // one workgroup per CU: 8 waves, 2 per SIMD
 constexpr int XB_MAX_WPG = 64;         // workgroups per group at most
+constexpr int XB_STAMPS = 8;
 constexpr int32_t ERR_XB = 1 << 21;    // an assumption of a block failed (speed bound, capacity, placement,
                                        // barrier time-out): the host rolls the chunk back and replays it with
                                        // the per-step kernels (never user-visible)
@@ -311,6 +312,11 @@ struct XbCtl {
     int32_t pad0[30];
     int32_t nload[XB_GROUPS];                // loaded bodies of each group (statistics, last launch)
     uint32_t vmax_bits;                      // float bits: max |v| at the start of the last launch (statistics)
+    uint32_t pad1[15];
+    // s_memrealtime (100 MHz) of each workgroup of the last launch at its
+    // phase ends (rb_diag_xb_stamps): start, speed bound, counts, map,
+    // copy, step 0, last step, end (committed)
+    unsigned long long stamp[XB_GROUPS * XB_MAX_WPG][XB_STAMPS];
 };
 enum : int32_t { XB_WHY_SPEED = 1, XB_WHY_CAP = 2, XB_WHY_PLACEMENT = 4, XB_WHY_TIMEOUT = 8 };
 template <typename T> struct XbParams {

@@ -125,6 +125,10 @@ void xblock_kernel(XbParams<T> P) {
     const int g = (int)(blockIdx.x % XB_GROUPS), r = (int)(blockIdx.x / XB_GROUPS), wpg = P.wpg;
     XbCtl *C = P.ctl;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    auto stamp = [&](int k) {
+        if (tid == 0) C->stamp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     const int64_t tmo = P.timeout_ticks;
     const int cap = P.cap;
     if (tid == 0) __hip_atomic_store(&C->xcc[blockIdx.x], xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -188,6 +192,7 @@ void xblock_kernel(XbParams<T> P) {
         }
     }
     xb_barrier(C, g, wpg, t0, tmo, P.err);
+    stamp(1);
     // the placement check: every workgroup of the group on one XCD
     if (tid < wpg && __hip_atomic_load(&C->xcc[g + XB_GROUPS * tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
                          __hip_atomic_load(&C->xcc[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -266,6 +271,7 @@ void xblock_kernel(XbParams<T> P) {
         C->cnt[g][r] = t;
     }
     xb_barrier(C, g, wpg, t0, tmo, P.err);
+    stamp(2);
     // offsets of this chunk's bodies in the copy (ascending ids)
     int off = 0, total = 0;
     for (int k = 0; k < wpg; ++k) {
@@ -289,6 +295,7 @@ void xblock_kernel(XbParams<T> P) {
     }
     if (r == 0 && tid == 0) C->nload[g] = total;
     xb_barrier(C, g, wpg, t0, tmo, P.err);
+    stamp(3);
 
     // ---- 3. each lane gathers the bodies it steps (waves dealt over the
     // group's workgroups in turn) and inserts them into step 0's table
@@ -338,6 +345,7 @@ void xblock_kernel(XbParams<T> P) {
         gtarget = (old / tot + 1ull) * tot;
     }
     xb_barrier(C, g, wpg, t0, tmo, P.err);
+    stamp(4);
 
     // ---- 4. K steps of the copy
     for (int s = 0; s < P.K; ++s) {
@@ -357,9 +365,11 @@ void xblock_kernel(XbParams<T> P) {
             }
         }
         if (bad) { atomicOr(&C->why, XB_WHY_SPEED); atomicOr(P.err, ERR_XB); }
+        if (s == 0) stamp(5);
         if (s + 1 < P.K) xb_barrier(C, g, wpg, t0, tmo, P.err);
     }
 
+    stamp(6);
     // ---- 5. commit the owned bodies, once every group has its copy
     if (tid == 0) {
         while (ld_sc1(&C->gathered[0]) < gtarget) {
@@ -386,6 +396,7 @@ void xblock_kernel(XbParams<T> P) {
     }
     // the group's next table generation (read by the next launch only)
     if (r == 0 && tid == 0) C->gen[g][0] = gen0 + (uint32_t)P.K + 1u;
+    stamp(7);
 }
 
 template <typename T> hipError_t launch_xblock(const XbParams<T> &p, int maxp, hipStream_t s) {

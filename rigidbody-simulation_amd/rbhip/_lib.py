@@ -64,6 +64,7 @@ SIGNATURES = {
     "rb_p2p_connect": (C.c_int, [_P, _P, _I64]),
     "rb_p2p_halo": (C.c_int, [_P, _I32]),
     "rb_shard_blocks": (C.c_int, [_P, _I32]),
+    "rb_diag_xb_stamps": (C.c_int, [_P, C.c_void_p, _I32, C.POINTER(_I32)]),
     "rb_record_contacts": (C.c_int, [_P, C.c_int]),
     "rb_get_contacts": (C.c_int, [_P, _P, _P, _P, _P, _I64, C.POINTER(_I64)]),
     "rb_kat_impulse": (C.c_int, [_I32, _I32, _I64, _P, _P]),

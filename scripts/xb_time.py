@@ -54,6 +54,20 @@ def main():
             wall = time.perf_counter() - t0
             times.append((e0.elapsed_time(e1) / a.steps * 1e3, wall / a.steps * 1e6))
         st = w.stats()
+        phases = None
+        if k > 0 and st["xb_steps"] > 0:
+            # the last launch's phase stamps (rb_diag_xb_stamps): median
+            # workgroup's time per phase, us
+            import ctypes
+            buf = np.zeros((512, 8), np.uint64)
+            wpg = ctypes.c_int32(0)
+            rbhip._lib.check(w._L.rb_diag_xb_stamps(w._h, buf.ctypes.data_as(ctypes.c_void_p), 512, ctypes.byref(wpg)),
+                             "rb_diag_xb_stamps")
+            b = buf[:8 * wpg.value].astype(np.int64)
+            d = np.diff(b, axis=1) / 100.0
+            names = ["bound", "counts", "map", "copy", "step0", "steps1..", "commit"]
+            phases = {nm: round(float(np.median(d[:, j])), 2) for j, nm in enumerate(names)}
+            phases["span"] = round(float((b[:, 7].max() - b[:, 0].min()) / 100.0), 2)
         q, v = w.get_state()
         w.close()
         if ref is None:
@@ -64,7 +78,8 @@ def main():
         wall = sorted(t[1] for t in times)
         rows.append({"K": k, "us_per_step_events_min": dev[0], "us_per_step_events_med": dev[len(dev) // 2],
                      "us_per_step_wall_med": wall[len(wall) // 2], "same_as_first": same,
-                     "xb_steps": st["xb_steps"], "xb_fallbacks": st["xb_fallbacks"], "form": st["form"]})
+                     "xb_steps": st["xb_steps"], "xb_fallbacks": st["xb_fallbacks"], "form": st["form"],
+                     "phases_us": phases})
         print(json.dumps(rows[-1]), flush=True)
     os.environ.pop("RBHIP_XB", None)
     os.environ.pop("RBHIP_XB_K", None)
