@@ -32,6 +32,63 @@
 #include "../../include/rbhip.h"
 #include "rb_internal.hpp"
 
+// Threads.  A graph capture on one thread's stream is invalidated by a
+// null-stream or device-wide call (hipMalloc, hipMemset, hipMemcpy, hipFree,
+// ...) that another thread makes meanwhile, and that call fails too (seen
+// with two threads creating, stepping and destroying their own worlds).  So
+// every entry point runs inside an ApiScope, and a capture (graph_replay)
+// inside a CaptureScope: a capture starts once no other thread is inside an
+// entry point (other than capturing too), and no entry point starts while a
+// capture runs.  Captures of several threads may overlap.
+namespace {
+struct Gate {
+    std::mutex m;
+    std::condition_variable cv;
+    int active = 0;      // threads inside an entry point, not capturing
+    int capturing = 0;   // threads inside a capture
+};
+Gate &gate() {
+    static Gate g;
+    return g;
+}
+thread_local int t_api_depth = 0;
+struct ApiScope {
+    ApiScope() {
+        if (t_api_depth++ == 0) {
+            std::unique_lock<std::mutex> l(gate().m);
+            gate().cv.wait(l, [] { return gate().capturing == 0; });
+            ++gate().active;
+        }
+    }
+    ~ApiScope() {
+        if (--t_api_depth == 0) {
+            std::lock_guard<std::mutex> l(gate().m);
+            --gate().active;
+            gate().cv.notify_all();
+        }
+    }
+    ApiScope(const ApiScope &) = delete;
+    ApiScope &operator=(const ApiScope &) = delete;
+};
+struct CaptureScope {   // (inside an ApiScope)
+    CaptureScope() {
+        std::unique_lock<std::mutex> l(gate().m);
+        --gate().active;
+        ++gate().capturing;
+        gate().cv.wait(l, [] { return gate().active == 0; });
+    }
+    ~CaptureScope() {
+        std::unique_lock<std::mutex> l(gate().m);
+        --gate().capturing;
+        gate().cv.notify_all();
+        gate().cv.wait(l, [] { return gate().capturing == 0; });
+        ++gate().active;
+    }
+    CaptureScope(const CaptureScope &) = delete;
+    CaptureScope &operator=(const CaptureScope &) = delete;
+};
+}  // namespace
+
 using namespace rb;
 
 static_assert(CK_SPHERE_BOX == RB_CK_SPHERE_BOX && CK_BOX_BOX0 == RB_CK_BOX_BOX0 && CK_BOX_EDGE == RB_CK_BOX_EDGE,
@@ -187,7 +244,10 @@ struct rb_world {
     uint64_t graph_tick = 0;
     // XCD-resident K-step blocks (rb_xblock.hip): sphere worlds
     // of the wide form on one rank
-    int xb_mode = -1;              // -1 auto, 0 off, 1 on (RBHIP_XB)
+    // 0 off (the default: at C3 the blocks measured 39 us per step against
+    // 16 us for the per-step kernels, profiles/r04/xb_time_c3.log), 1 on,
+    // -1 auto (RBHIP_XB=-1: worlds of >= RBHIP_XB_MIN_BODIES)
+    int xb_mode = 0;
     int xb_k = 8;                  // steps per launch (RBHIP_XB_K)
     int xb_wpg = 0;                // workgroups per group (CUs / 8; 0: the device cannot run the blocks)
     int64_t xb_min_bodies = 32768; // auto mode: fewer bodies step with the per-step kernels
@@ -712,7 +772,9 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
         // capture both parities at once, so later calls starting at either
         // replay without a capture (a parity still cached is kept; both
         // entries get the current tick, so the one not launched now is not
-        // the first evicted)
+        // the first evicted).  No other thread inside the library meanwhile
+        // (CaptureScope).
+        CaptureScope capture_scope_;
         for (int c0 = 0; c0 < 2; ++c0) {
             const auto k0 = std::make_tuple(K, c0, dt, e, mu, thr, variant);
             auto old = w->graphs.find(k0);
@@ -1530,6 +1592,7 @@ const char *rb_last_error(void) { return g_err.c_str(); }
 const char *rb_version(void) { return "librbhip 0.2 (gfx950, HIP)"; }
 
 int rb_world_create(rb_world **out, const rb_scene_desc *d) {
+    ApiScope api_scope_;
     if (!out || !d) return fail(RB_EINVAL, "null argument");
     *out = nullptr;
     if (d->n_bodies <= 0 || d->n_bodies > (int64_t)INT32_MAX / 2) return fail(RB_EINVAL, "n_bodies out of range");
@@ -1586,9 +1649,9 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_HELP")) w->wide_help = atoi(ev) != 0;
-    // XCD-resident K-step blocks (rb_xblock.hip): RBHIP_XB = 0 off, 1 on,
-    // unset auto (sphere worlds of the wide form, >= RBHIP_XB_MIN_BODIES)
-    if (const char *ev = getenv("RBHIP_XB")) w->xb_mode = atoi(ev) ? 1 : 0;
+    // XCD-resident K-step blocks (rb_xblock.hip): RBHIP_XB = 0 off (default),
+    // 1 on, -1 auto (sphere worlds of >= RBHIP_XB_MIN_BODIES)
+    if (const char *ev = getenv("RBHIP_XB")) w->xb_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_XB_K")) w->xb_k = std::max(1, std::min(64, atoi(ev)));
     if (const char *ev = getenv("RBHIP_XB_MIN_BODIES")) w->xb_min_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_XB_VALPHA")) w->xb_valpha = atof(ev);
@@ -1735,6 +1798,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
 }
 
 void rb_world_destroy(rb_world *w) {
+    ApiScope api_scope_;
     if (w && w->xb_pending) {
         (void)hipSetDevice(w->device);
         (void)hipStreamSynchronize(w->stream);
@@ -1743,6 +1807,7 @@ void rb_world_destroy(rb_world *w) {
 }
 
 int rb_set_stream(rb_world *w, void *s) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     // work queued on the old stream (a block run's check included)
@@ -1825,6 +1890,7 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
 }
 
 int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
+    ApiScope api_scope_;
     if (!w || !qpos || !qvel) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1857,6 +1923,7 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
 }
 
 int rb_get_state(rb_world *w, double *qpos, double *qvel) {
+    ApiScope api_scope_;
     if (!w || (!qpos && !qvel)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1876,6 +1943,7 @@ int rb_get_state(rb_world *w, double *qpos, double *qvel) {
 }
 
 int rb_set_xfrc(rb_world *w, const double *xf) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1899,11 +1967,13 @@ int rb_set_xfrc(rb_world *w, const double *xf) {
 }
 
 int rb_step_async(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     return enqueue_steps(w, nsteps, dt, e, mu, thr);
 }
 
 int rb_sync(rb_world *w) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1911,6 +1981,7 @@ int rb_sync(rb_world *w) {
 }
 
 int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    ApiScope api_scope_;
     if (w) w->sync_call = true;
     int rc = rb_step_async(w, nsteps, dt, e, mu, thr);
     if (w) w->sync_call = false;
@@ -1920,6 +1991,7 @@ int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double 
 }
 
 int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (w->law != RB_LAW_MUJOCO) return fail(RB_EUNSUPPORTED, "sharded stepping supports the default contact law only");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0)) return fail(RB_EINVAL, "invalid step parameters");
@@ -1932,6 +2004,7 @@ int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
 }
 
 int rb_shard_exchange_done(rb_world *w) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     // insert every body not owned here into the next table (own ones went in
@@ -1946,6 +2019,7 @@ int rb_shard_exchange_done(rb_world *w) {
 }
 
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (dev_ptr) *dev_ptr = w->snap[1 - w->sp()];
     if (shard_elems) *shard_elems = 4 * w->S;
@@ -1954,6 +2028,7 @@ int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *e
 }
 
 int rb_gquat_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (dev_ptr) *dev_ptr = w->boxes ? w->qsnap[1 - w->sp()] : nullptr;
     if (shard_elems) *shard_elems = w->boxes ? 4 * w->S : 0;
@@ -1962,6 +2037,7 @@ int rb_gquat_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *
 }
 
 int rb_comm_unique_id(void *id, int32_t bytes) {
+    ApiScope api_scope_;
     if (!id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
     if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
     ncclUniqueId u;
@@ -1972,6 +2048,7 @@ int rb_comm_unique_id(void *id, int32_t bytes) {
 }
 
 int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
+    ApiScope api_scope_;
     if (!w || !id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "null world or short id");
     if (w->comm) return fail(RB_EINVAL, "communicator already initialised");
     if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
@@ -1993,6 +2070,7 @@ int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
 int p2p_nhandles(const rb_world *w) { return w->boxes ? 5 : 3; }
 
 int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
+    ApiScope api_scope_;
     if (!w || !len) return fail(RB_EINVAL, "null argument");
     const int nh = p2p_nhandles(w);
     const int64_t need = nh * (int64_t)sizeof(hipIpcMemHandle_t);
@@ -2023,6 +2101,7 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
 }
 
 int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
+    ApiScope api_scope_;
     if (!w || !all) return fail(RB_EINVAL, "null argument");
     const int nh = p2p_nhandles(w);
     const int64_t blob = nh * (int64_t)sizeof(hipIpcMemHandle_t);
@@ -2075,6 +2154,7 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
 
 // diagnostic: the last block launch's phase stamps, [workgroups][8]
 int rb_diag_xb_stamps(rb_world *w, uint64_t *out, int32_t n_wg, int32_t *wpg) {
+    ApiScope api_scope_;
     if (!w || !out) return fail(RB_EINVAL, "null argument");
     if (!w->xb_ctl) return fail(RB_EINVAL, "no block launch yet");
     HIPCHK(hipSetDevice(w->device));
@@ -2088,6 +2168,7 @@ int rb_diag_xb_stamps(rb_world *w, uint64_t *out, int32_t n_wg, int32_t *wpg) {
 // Sharded K-step blocks (XS): every rank of a peer-to-peer world
 // alike.  The buffers are made at the first enable.
 int rb_shard_blocks(rb_world *w, int32_t mode) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (mode != 0 && mode != 1) return fail(RB_EINVAL, "mode must be 0 or 1");
     HIPCHK(hipSetDevice(w->device));
@@ -2118,6 +2199,7 @@ int rb_shard_blocks(rb_world *w, int32_t mode) {
 }
 
 int rb_p2p_halo(rb_world *w, int32_t enable) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (!w->p2p) return fail(RB_EINVAL, "rb_p2p_halo before rb_p2p_connect");
     HIPCHK(hipSetDevice(w->device));
@@ -2141,11 +2223,13 @@ int rb_p2p_halo(rb_world *w, int32_t enable) {
 }
 
 int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     return enqueue_steps(w, nsteps, dt, e, mu, thr, true);
 }
 
 int rb_record_contacts(rb_world *w, int enable) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -2164,6 +2248,7 @@ int rb_record_contacts(rb_world *w, int enable) {
 
 int rb_get_contacts(rb_world *w, int32_t *counts, int32_t *partner, int32_t *kind, double *dist, int64_t cap,
                     int64_t *total) {
+    ApiScope api_scope_;
     if (!w || !counts) return fail(RB_EINVAL, "null argument");
     if (!w->rec_count) return fail(RB_EINVAL, "contact recording was never enabled");
     HIPCHK(hipSetDevice(w->device));
@@ -2227,26 +2312,32 @@ static int kat_common(int32_t device, int32_t dtype, int64_t n, const double *in
 }
 
 int rb_kat_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    ApiScope api_scope_;
     return kat_common(device, dtype, n, in, out, 24, 10, 0);
 }
 
 int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    ApiScope api_scope_;
     return kat_common(device, dtype, n, in, out, 7, 18, 1);
 }
 
 int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    ApiScope api_scope_;
     return kat_common(device, dtype, n, in, out, 26, 6, 2);
 }
 
 int rb_kat_pair_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    ApiScope api_scope_;
     return kat_common(device, dtype, n, in, out, 27, 3, 3);
 }
 
 int rb_kat_narrow(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
+    ApiScope api_scope_;
     return kat_common(device, dtype, n, in, out, 22, 33, 4);
 }
 
 int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (law != RB_LAW_MUJOCO && law != RB_LAW_BALLS) return fail(RB_EINVAL, "unknown contact law %d", law);
     if (!(tol >= 0) || !(tol < 1e6)) return fail(RB_EINVAL, "tol must be finite and >= 0");
@@ -2311,6 +2402,7 @@ extern "C" {
 // XCD-resident blocks (rb_xblock.hip) replace them.  The entry stays for ABI
 // compatibility: mode -1 / 0 are accepted (nothing to configure), 1 fails.
 int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (mode < -1 || mode > 1 || kmax < 0 || kmax > 64 || !(band >= 0) || owned < 0)
         return fail(RB_EINVAL, "bad tile configuration");
@@ -2319,6 +2411,7 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 }
 
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
+    ApiScope api_scope_;
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -2332,6 +2425,7 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
 }
 
 int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     if (n_owned) *n_owned = w->n_local;
     if (bytes) *bytes = w->bytes_per_body_step;
@@ -2339,6 +2433,7 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {
 }
 
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches) {
+    ApiScope api_scope_;
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     int rc = collect_timing(w);

@@ -332,6 +332,10 @@ template <typename T> struct Lead {
 };
 #define LEAD_ARGS(p) (p).snap_cur, (p).st.base, (p).st.S, (p).cs.base, (p).cs.Npad, (p).cs.kind, (p).n_local, (p).lo
 
+#ifndef RB_SOLVE_PIPE
+#define RB_SOLVE_PIPE 1
+#endif
+
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 template <typename T>
 __device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T m, LazyInvI<T> &invI, V3<T> &v,
@@ -409,9 +413,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // a time: each unrolled copy of the loop body inlines the box
     // narrowphase (4 copies made the kernel 169 KB)
     constexpr int PB = BOXES ? 1 : 4;
-    for (int s0 = 0; s0 < np_; s0 += PB) {
-        int32_t jj[PB];
-        Snap<T> pe[PB];
+    auto fetch = [&](int s0, int32_t (&jj)[PB], Snap<T> (&pe)[PB]) {
 #pragma unroll
         for (int u = 0; u < PB; ++u)
             if (s0 + u < np_) jj[u] = pid[CHK((s0 + u) * stride, 32 * stride)];
@@ -426,6 +428,25 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             } else {
                 pe[u] = xld(p.snap_cur + CHK(jj[u], p.n_global));
             }
+        }
+    };
+    // sphere kernels (RB_SOLVE_PIPE): the next batch's snapshots load under
+    // this batch's solves — a body with many partners (C4's pile-ups: up to
+    // 28) otherwise waits one round trip per PB partners re-read from memory
+    [[maybe_unused]] int32_t jn[PB];
+    [[maybe_unused]] Snap<T> sn_next[PB];
+    constexpr bool pipe = !BOXES && RB_SOLVE_PIPE && PM != 1;   // (the cooperative form: LDS only)
+    if constexpr (pipe)
+        if (np_ > 0) fetch(0, jn, sn_next);
+    for (int s0 = 0; s0 < np_; s0 += PB) {
+        int32_t jj[PB];
+        Snap<T> pe[PB];
+        if constexpr (pipe) {
+#pragma unroll
+            for (int u = 0; u < PB; ++u) { jj[u] = jn[u]; pe[u] = sn_next[u]; }
+            if (s0 + PB < np_) fetch(s0 + PB, jn, sn_next);
+        } else {
+            fetch(s0, jj, pe);
         }
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
