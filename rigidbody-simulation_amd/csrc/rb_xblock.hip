@@ -39,7 +39,11 @@
 // over every body at the launch's start (each group scans all of them).
 #define RB_XB 1
 #undef RB_STAMPS
-#define RB_STAMPS 0              // (diagnostic stamp builds: the buffer lives in rb_kernels.hip's own unit)
+#if RB_XB_STAMPS                 // diagnostic build: the body code's phase stamps, this unit's own buffer
+#define RB_STAMPS 1
+#else
+#define RB_STAMPS 0              // (stamp builds of the per-step kernels: their buffer lives in their own unit)
+#endif
 #define RB_STEP_BLOCK 512        // (rb_internal.hpp XB_THREADS): the wide form's LDS columns
 #define RB_WIDE_LDSPOS 0         // partner snapshots re-read in the solve (L2-resident here)
 #define RB_WIDE_QBATCH 8         // candidates per round trip: two waves per SIMD must fit in 256 registers
@@ -411,6 +415,13 @@ template <typename T> hipError_t launch_xblock(const XbParams<T> &p, int maxp, h
     }
     return hipGetLastError();
 }
+
+#if RB_XB_STAMPS
+// the last step's stamps of wave 0 of every workgroup (scripts/stamps_c4.py reads 16 per block)
+extern "C" int rb_diag_stamps(unsigned long long *out, int nblocks) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 16 * nblocks);
+}
+#endif
 
 template hipError_t launch_xblock<double>(const XbParams<double> &, int, hipStream_t);
 template hipError_t launch_xblock<float>(const XbParams<float> &, int, hipStream_t);

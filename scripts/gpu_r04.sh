@@ -28,6 +28,8 @@ for step in "$@"; do
         c4ab) run c4_pipe_ab 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline \
               SIZES=256x256 WARM=500 ENVS=RBHIP_XB=0 ROUNDS=2 python -u scripts/ablate.py ;;
         xsmp) run xs_mp 600 python -u -m pytest tests/test_gpu_shard_mp.py -x -v -k "sharded_blocks or two_process_shards_match_single_world and p2p" --timeout 300 --timeout-method thread ;;
+        xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
+        xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
         stampsc4) run stamps_c4 300 python -u scripts/stamps_c4.py --warm 700 ;;
         framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
         pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
