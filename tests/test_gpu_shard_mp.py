@@ -84,8 +84,10 @@ def _blocks_worker(rank, P, port, out, patch, chunks, halo):
     for pth in (ROOT, PKG):
         sys.path.insert(0, pth)
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
-    # two ranks' block launches share the one GPU: 16 workgroups per XCD each
-    os.environ["RBHIP_XB_WPG"] = "16"
+    # the ranks' block launches share the one GPU: 32 / P workgroups per XCD
+    # each, so that they all fit on it at once (a launch waits at its
+    # barriers for all of its own workgroups)
+    os.environ["RBHIP_XB_WPG"] = str(32 // P)
     os.environ["RBHIP_XB_K"] = "6"
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=P)
