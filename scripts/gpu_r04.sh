@@ -28,6 +28,7 @@ for step in "$@"; do
         c4ab) run c4_pipe_ab 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline \
               SIZES=256x256 WARM=500 ENVS=RBHIP_XB=0 ROUNDS=2 python -u scripts/ablate.py ;;
         xsmp) run xs_mp 600 python -u -m pytest tests/test_gpu_shard_mp.py -x -v -k "sharded_blocks or two_process_shards_match_single_world and p2p" --timeout 300 --timeout-method thread ;;
+        atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
         stampsc4) run stamps_c4 300 python -u scripts/stamps_c4.py --warm 700 ;;
