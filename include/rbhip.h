@@ -337,7 +337,9 @@ int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t
 #define RB_STAT_XB_ON        26   /* a long rb_step would use the blocks now */
 #define RB_STAT_IO_SKIPPED   27   /* rb_set_state calls that were no-ops (the bytes rb_get_state handed out) */
 #define RB_STAT_IO_UPLOADS   28   /* rb_set_state calls that uploaded          */
-#define RB_STATS_COUNT       29
+#define RB_STAT_XB_WHY       29   /* why bits of the block runs rolled back (OR; 1 speed, 2 capacity,
+                                     4 placement, 8 time-out, 16 other error) */
+#define RB_STATS_COUNT       30
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

@@ -271,6 +271,7 @@ struct rb_world {
     int64_t xb_stats[4] = {};      // runs, launches, steps committed, runs rolled back and replayed per step
     int32_t xb_backoff = 0;        // eligible runs to skip after a roll-back (doubles)
     int32_t xb_skip = 0;
+    int32_t xb_why = 0;            // XB_WHY_* of the runs rolled back (OR), 16: another error bit
     bool xb_sharded = false;       // the pending run is a sharded one (XS)
     // sharded K-step blocks (XS: rb_p2p.hip xs_push_kernel + the blocks'
     // sharded form): peer-to-peer worlds, every rank alike
@@ -1268,6 +1269,7 @@ int xb_finish(rb_world *w) {
     // (a shard: every rank rolled back alike — the push kernels spread an
     // error to every rank — and must keep deciding alike, so only the
     // back-off, which every rank advances the same way, applies)
+    w->xb_why |= ctl.why | ((err & ~ERR_XB) ? 16 : 0);
     if (!w->xb_sharded && (ctl.why & (XB_WHY_PLACEMENT | XB_WHY_TIMEOUT))) w->xb_mode = 0;
     w->xb_backoff = w->xb_backoff ? std::min(2 * w->xb_backoff, 64) : 1;
     w->xb_skip = w->xb_backoff;
@@ -2419,7 +2421,8 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), 0, 0, 0, 0, 0, 0, 0, form, 0, 0, 0, 0, 0, 0,
                                        w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H,
                                        (int64_t)w->maxp, w->xb_stats[0], w->xb_stats[1], w->xb_stats[2], w->xb_stats[3],
-                                       (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0, w->io_stats[0], w->io_stats[1]};
+                                       (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0, w->io_stats[0], w->io_stats[1],
+                                       (int64_t)w->xb_why};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

@@ -72,12 +72,13 @@ __device__ __forceinline__ int64_t chk(int64_t idx, int64_t n, int line) {
 #define RB_XB 0
 #endif
 // XCD-resident loads: 1 = sc1 (agent-scope relaxed atomic loads, 8 bytes
-// each), 2 = nt 16-byte loads
+// each), 2 = nt 16-byte loads, 0 = plain loads (L1-cached: the block kernel
+// then invalidates each CU's L1 after every barrier, rb_xblock.hip)
 #ifndef RB_XB_LD
 #define RB_XB_LD 1
 #endif
 template <typename V> __device__ __forceinline__ V xld(const V *p) {
-#if RB_XB
+#if RB_XB && RB_XB_LD != 0
     static_assert(sizeof(V) % 4 == 0, "xld: whole words");
     V v;
     if constexpr (RB_XB_LD == 2 && sizeof(V) % 16 == 0) {

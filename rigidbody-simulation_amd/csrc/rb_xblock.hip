@@ -83,6 +83,11 @@ __device__ __forceinline__ void xb_barrier(XbCtl *C, int g, int wpg, unsigned lo
             }
             __builtin_amdgcn_s_sleep(1);
         }
+#if RB_XB_LD == 0
+        // plain (L1-cached) loads in the steps: this CU's L1 may hold lines
+        // other CUs of the XCD have since rewritten in the L2
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     }
     __syncthreads();
 }

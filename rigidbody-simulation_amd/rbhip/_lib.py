@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librbhip.so")
+# RBHIP_LIB_PATH: a diagnostic build of the same library (A/B runs)
+LIB_PATH = os.environ.get("RBHIP_LIB_PATH") or os.path.join(HERE, "librbhip.so")
 
 RB_OK = 0
 ERRNAMES = {-22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -75: "EOVERFLOW", -95: "EUNSUPPORTED",
@@ -84,7 +85,7 @@ STAT_NAMES = ["graphs", "tile_runs", "tile_blocks", "tile_redo_taint", "tile_red
               "tile_fallback", "tile_steps", "form", "tiles", "tile_threads", "tile_kmax", "tile_cap",
               "tile_size_um", "tile_on", "box_opt_chunks", "box_rollbacks", "refits",
               "table_grows", "buckets", "max_partners", "xb_runs", "xb_launches", "xb_steps",
-              "xb_fallbacks", "xb_k", "xb_on", "io_skipped", "io_uploads"]
+              "xb_fallbacks", "xb_k", "xb_on", "io_skipped", "io_uploads", "xb_why"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
               3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help"}
 

@@ -28,6 +28,10 @@ for step in "$@"; do
         c4ab) run c4_pipe_ab 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline \
               SIZES=256x256 WARM=500 ENVS=RBHIP_XB=0 ROUNDS=2 python -u scripts/ablate.py ;;
         xsmp) run xs_mp 600 python -u -m pytest tests/test_gpu_shard_mp.py -x -v -k "sharded_blocks or two_process_shards_match_single_world and p2p" --timeout 300 --timeout-method thread ;;
+        xbl1) run xb_tests_l1 600 env RBHIP_LIB_PATH=build/xb_l1.so python -u -m pytest tests/test_gpu_xblock.py -x -q --timeout 300 --timeout-method thread &&
+              run xb_time_l1 300 env RBHIP_LIB_PATH=build/xb_l1.so python -u scripts/xb_time.py --ks 0,8,16 &&
+              run xb_time_l1_8k 300 env RBHIP_LIB_PATH=build/xb_l1.so python -u scripts/xb_time.py --config slab8k --ks 0,8,16 &&
+              run xb_stamps_l1 300 python -u scripts/xb_stamps.py --lib build/xbstamps_l1.so --config c3 --k 8 ;;
         atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;

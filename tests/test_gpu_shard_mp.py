@@ -87,7 +87,7 @@ def _blocks_worker(rank, P, port, out, patch, chunks, halo):
     # the ranks' block launches share the one GPU: 32 / P workgroups per XCD
     # each, so that they all fit on it at once (a launch waits at its
     # barriers for all of its own workgroups)
-    os.environ["RBHIP_XB_WPG"] = str(32 // P)
+    os.environ["RBHIP_XB_WPG"] = str(32 // P - 2 * (P - 2))     # 16 at P = 2, 8 at P = 3
     os.environ["RBHIP_XB_K"] = "6"
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=P)
@@ -102,7 +102,7 @@ def _blocks_worker(rank, P, port, out, patch, chunks, halo):
     q, v = sw.gather_state()
     if rank == 0:
         np.save(out, np.concatenate([q, v], axis=1))
-        np.save(out + ".stats.npy", np.array([st["xb_steps"], st["xb_fallbacks"], st["xb_runs"]]))
+        np.save(out + ".stats.npy", np.array([st["xb_steps"], st["xb_fallbacks"], st["xb_runs"], st["xb_why"]]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -126,10 +126,10 @@ def test_sharded_blocks_match_single_world(tmp_path, P, patch, halo, chunks):
     mp.start_processes(_blocks_worker, args=(P, _free_port(), out, patch, chunks, halo), nprocs=P,
                        start_method="spawn")
     got = np.load(out)
-    steps, fallbacks, runs = np.load(out + ".stats.npy")
+    steps, fallbacks, runs, why = np.load(out + ".stats.npy")
     assert np.array_equal(got[:, :7].view(np.uint64), q1.view(np.uint64))
     assert np.array_equal(got[:, 7:].view(np.uint64), v1.view(np.uint64))
-    assert fallbacks == 0 and steps == sum(n for n in chunks if n >= 2), (steps, fallbacks, runs)
+    assert fallbacks == 0 and steps == sum(n for n in chunks if n >= 2), (steps, fallbacks, runs, why)
 
 
 # ---------------------------------------------------------------- in-library RCCL exchange
