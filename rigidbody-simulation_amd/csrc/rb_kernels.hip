@@ -1096,6 +1096,14 @@ __global__ __launch_bounds__(64) void kat_narrow_kernel(int64_t n, const double 
 }
 
 // ---- launchers ----------------------------------------------------------
+// The wide form's kernels live in their own unit (RB_WIDE_UNIT=1, built with
+// the memory-clause scheduling flags): the other units must call that unit's
+// instantiation, not compile (and, through the linker's choice among weak
+// copies, possibly run) a copy of their own
+#if defined(RB_WIDE_UNIT) && RB_WIDE_UNIT == 0
+extern template hipError_t launch_step_wide<double>(const StepParams<double> &, int, bool, hipStream_t);
+extern template hipError_t launch_step_wide<float>(const StepParams<float> &, int, bool, hipStream_t);
+#endif
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s) {
     const bool coop = form == FORM_COOP || form == FORM_COOP_HELP;
     const int nb = coop ? STEP_BLOCK / 8 : STEP_BLOCK;

@@ -32,6 +32,10 @@ for step in "$@"; do
               run xb_time_l1 300 env RBHIP_LIB_PATH=build/xb_l1.so python -u scripts/xb_time.py --ks 0,8,16 &&
               run xb_time_l1_8k 300 env RBHIP_LIB_PATH=build/xb_l1.so python -u scripts/xb_time.py --config slab8k --ks 0,8,16 &&
               run xb_stamps_l1 300 python -u scripts/xb_stamps.py --lib build/xbstamps_l1.so --config c3 --k 8 ;;
+        linkab) run link_ab_c3 300 env "LIBS=build/ab_oldlink.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=flat \
+              SIZES=256x256,128x256,256x32 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
+              run link_ab_c4 300 env "LIBS=build/ab_oldlink.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
+              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
         atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
