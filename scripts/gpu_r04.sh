@@ -36,9 +36,9 @@ for step in "$@"; do
               SIZES=256x256,128x256,256x32 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
               run link_ab_c4 300 env "LIBS=build/ab_oldlink.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
               SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
-        spab) run slotpos_ab_c3 300 env "ENVS=RBHIP_SLOTPOS=1;RBHIP_SLOTPOS=0" SCENE=flat SIZES=256x256,128x256 WARM=20 \
+        spab) run slotpos_ab_c3 300 env LIBS=rigidbody-simulation_amd/rbhip/librbhip.so "ENVS=RBHIP_SLOTPOS=1;RBHIP_SLOTPOS=0" SCENE=flat SIZES=256x256,128x256 WARM=20 \
               ROUNDS=3 python -u scripts/ablate.py &&
-              run slotpos_ab_c4 300 env "ENVS=RBHIP_SLOTPOS=1;RBHIP_SLOTPOS=0" SCENE=incline SIZES=256x256 WARM=500 \
+              run slotpos_ab_c4 300 env LIBS=rigidbody-simulation_amd/rbhip/librbhip.so "ENVS=RBHIP_SLOTPOS=1;RBHIP_SLOTPOS=0" SCENE=incline SIZES=256x256 WARM=500 \
               ROUNDS=2 python -u scripts/ablate.py ;;
         atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
