@@ -272,7 +272,6 @@ struct rb_world {
     int32_t xb_backoff = 0;        // eligible runs to skip after a roll-back (doubles)
     int32_t xb_skip = 0;
     int32_t xb_why = 0;            // XB_WHY_* of the runs rolled back (OR), 16: another error bit
-    int slotpos_mode = -1;         // the wide form's slot snapshots: 1 on, 0 off, -1 from a growth to 32 partners
     bool xb_sharded = false;       // the pending run is a sharded one (XS)
     // sharded K-step blocks (XS: rb_p2p.hip xs_push_kernel + the blocks'
     // sharded form): peer-to-peer worlds, every rank alike
@@ -692,11 +691,10 @@ int chunk_restore(rb_world *w) {
 // the wide form's slot snapshots (rb_grid.hpp WIDE_SLOTPOS): a candidate's
 // position from its bucket's contiguous slot block instead of a gather by id
 // (C4's pile-ups: the gathers by id were the step's cost)
-// Kept only where it pays (RBHIP_SLOTPOS: 1 always, 0 never, unset: from
-// the first growth to 32 partners, i.e. a pile-up): at C3, one body per cell,
-// the copies cost a scattered 32-B write per body-step and save nothing.
 bool wide_slotpos(const rb_world *w, bool coop, bool split, int64_t H) {
-    if (!WIDE_SLOTPOS || coop || split || w->slotpos_mode == 0) return false;
+    if (!WIDE_SLOTPOS || coop || split) return false;
+    if (const char *ev = getenv("RBHIP_SLOTPOS"))
+        if (atoi(ev) == 0) return false;
     int64_t cap = int64_t(8) << 30;
     if (const char *ev = getenv("RBHIP_SLOTPOS_MAX_BYTES")) cap = atoll(ev);
     return 2 * (int64_t)w->esz * 4 * LINE_WORDS * H <= cap;
@@ -742,12 +740,6 @@ int grow_partners(rb_world *w) {
     drop_graphs(w);                                   // the instantiation is chosen at capture
     w->maxp = 32;
     w->maxrec = 4 * w->n_planes + (w->boxes ? 4 : 1) * w->maxp;
-    // a pile-up: the wide form's candidates from slot snapshots from now on
-    // (the tables are rebuilt with them at the replay's prime)
-    if (w->slotpos_mode < 0 && !w->pos[0] && w->n_local > w->coop_max && !w->plist && wide_slotpos(w, false, false, w->H)) {
-        for (int k = 0; k < 2; ++k) HIPCHK(hipMalloc(&w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H));
-        w->primed = false;
-    }
     if (w->rec_count) {
         const size_t slots = (size_t)w->maxrec * (w->S > 0 ? w->S : 1);
         void *old[] = {w->rec_partner, w->rec_kind, w->rec_dist};
@@ -1677,7 +1669,6 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // 1 on, -1 auto (sphere worlds of >= RBHIP_XB_MIN_BODIES)
     if (const char *ev = getenv("RBHIP_XB")) w->xb_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_XB_K")) w->xb_k = std::max(1, std::min(64, atoi(ev)));
-    if (const char *ev = getenv("RBHIP_SLOTPOS")) w->slotpos_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_XB_MIN_BODIES")) w->xb_min_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_XB_VALPHA")) w->xb_valpha = atof(ev);
     if (const char *ev = getenv("RBHIP_XB_VBETA")) w->xb_vbeta = atof(ev);
@@ -1796,7 +1787,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         // slot snapshots feed the cooperative search, and the wide form's
         // candidate gathers (rb_grid.hpp WIDE_SLOTPOS) while both tables'
         // copies fit in RBHIP_SLOTPOS_MAX_BYTES (RBHIP_SLOTPOS=0: not kept)
-        if (needs_slot_snapshots(coop, split) || (w->slotpos_mode == 1 && wide_slotpos(w, coop, split, w->H)))
+        if (needs_slot_snapshots(coop, split) || wide_slotpos(w, coop, split, w->H))
             ALLOC(w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H);
     }
     ALLOC(w->err, sizeof(int32_t));
