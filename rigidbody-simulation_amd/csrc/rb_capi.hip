@@ -688,18 +688,6 @@ int chunk_restore(rb_world *w) {
     w->primed = false;
     return RB_OK;
 }
-// the wide form's slot snapshots (rb_grid.hpp WIDE_SLOTPOS): a candidate's
-// position from its bucket's contiguous slot block instead of a gather by id
-// (C4's pile-ups: the gathers by id were the step's cost)
-bool wide_slotpos(const rb_world *w, bool coop, bool split, int64_t H) {
-    if (!WIDE_SLOTPOS || coop || split) return false;
-    if (const char *ev = getenv("RBHIP_SLOTPOS"))
-        if (atoi(ev) == 0) return false;
-    int64_t cap = int64_t(8) << 30;
-    if (const char *ev = getenv("RBHIP_SLOTPOS_MAX_BYTES")) cap = atoll(ev);
-    return 2 * (int64_t)w->esz * 4 * LINE_WORDS * H <= cap;
-}
-
 // twice the buckets (both tables, emptied), if under the world's limit; the
 // linear layout's period gets the extra bit (refit_from_device re-splits it)
 int grow_table(rb_world *w, bool &grown) {
@@ -716,9 +704,7 @@ int grow_table(rb_world *w, bool &grown) {
         if (w->pos[k]) {
             HIPCHK(hipFree(w->pos[k]));
             w->pos[k] = nullptr;
-            // (the wide form's copies only while they fit the cap)
-            if (w->n_local <= w->coop_max || wide_slotpos(w, false, false, H))
-                HIPCHK(hipMalloc(&w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * H));
+            HIPCHK(hipMalloc(&w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * H));
         }
     }
     w->H = H;
@@ -1784,11 +1770,8 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     for (int k = 0; k < 2; ++k) {
         ALLOC(w->ids[k], sizeof(uint32_t) * LINE_WORDS * w->H);
         ALLOC(w->spill[k], sizeof(uint32_t) * (2 + 2 * SPILL_CAP));
-        // slot snapshots feed the cooperative search, and the wide form's
-        // candidate gathers (rb_grid.hpp WIDE_SLOTPOS) while both tables'
-        // copies fit in RBHIP_SLOTPOS_MAX_BYTES (RBHIP_SLOTPOS=0: not kept)
-        if (needs_slot_snapshots(coop, split) || wide_slotpos(w, coop, split, w->H))
-            ALLOC(w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H);
+        // slot snapshots feed the cooperative search only
+        if (needs_slot_snapshots(coop, split)) ALLOC(w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H);
     }
     ALLOC(w->err, sizeof(int32_t));
 #undef ALLOC

@@ -525,7 +525,6 @@ constexpr int WIDE_HEAD_IDS = 6;                    // (heads are at least 32 by
 #endif
 constexpr int WIDE_QBATCH = RB_WIDE_QBATCH;         // candidates per round trip (8: C3 15.9 us, 32k 12.8; 12: 15.6, 12.3; 16 spills)
 constexpr int WIDE_MAXC = 8 * WIDE_HEAD_IDS;        // head candidates listed in LDS
-// (WIDE_SLOTPOS, rb_internal.hpp: candidates' positions from slot snapshots)
 struct Head6 { uint4 a, b; };
 template <typename T>
 __device__ __forceinline__ Head6 bucket_head6(const Table<T> &tab, uint32_t b, int rl) {
@@ -547,9 +546,9 @@ template <int S> __device__ __forceinline__ uint32_t head6_id(const Head6 &h) {
 template <typename T, int MAXP, typename Hit, typename Overlap>
 __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
                                                        uint32_t *s_cand, uint8_t *s_didx, Snap<T> *s_hpos, int tid,
-                                                       uint32_t gen, Hit hit, Overlap overlap, uint8_t *s_ks = nullptr) {
+                                                       uint32_t gen, Hit hit, Overlap overlap) {
     constexpr int NB = STEP_BLOCK;
-    constexpr int QB = MAXP > 16 ? 8 : WIDE_QBATCH;   // (32 partners: the registers of 12 do not fit)
+    constexpr int QB = WIDE_QBATCH;
     int32_t cx, cy, cz, sx, sy, sz;
     if (!neighbourhood(p, x, cx, cy, cz, sx, sy, sz)) {
         atomicOr(p.err, ERR_DOMAIN);
@@ -587,7 +586,6 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
         {                                                                         \
             const uint32_t t = head6_id<S>(hd[k]);                                \
             s_cand[n * NB + tid] = t;                                             \
-            if (WIDE_SLOTPOS) s_ks[n * NB + tid] = (uint8_t)((k << 3) | S);        \
             n += (S < m && (t & ~BOX_FLAG) != (uint32_t)i) ? 1 : 0;               \
         }
         RB_WIDE_LIST(0) RB_WIDE_LIST(1) RB_WIDE_LIST(2) RB_WIDE_LIST(3) RB_WIDE_LIST(4) RB_WIDE_LIST(5)
@@ -599,19 +597,6 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     // lane (padding = the body itself, which loads nothing): measured 2-7 %
     // faster at 32k-65k bodies than a loop all of whose batches are
     // conditional on the lane's candidate count
-    // slot snapshots (the table keeps a copy of each id's step-start
-    // snapshot beside it, Table::pos): a candidate's position comes from its
-    // bucket's contiguous slot block instead of a gather by id — the lines a
-    // crowded neighbourhood reads are its buckets', not one per candidate
-    const bool slotpos = WIDE_SLOTPOS && p.cur.pos != nullptr;
-    auto bucket_k = [&](uint32_t k) {
-        // a select tree over the eight bucket indices (no dynamically
-        // indexed register array: it would live in scratch)
-        const uint32_t b01 = (k & 1) ? b[1] : b[0], b23 = (k & 1) ? b[3] : b[2];
-        const uint32_t b45 = (k & 1) ? b[5] : b[4], b67 = (k & 1) ? b[7] : b[6];
-        const uint32_t b03 = (k & 2) ? b23 : b01, b47 = (k & 2) ? b67 : b45;
-        return (k & 4) ? b47 : b03;
-    };
     auto batch = [&](int base) {
         uint32_t tj[QB];
         Snap<T> sn[QB];
@@ -620,14 +605,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
             sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
-            if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) {
-                const Snap<T> *src = p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global);
-                if (WIDE_SLOTPOS && slotpos) {
-                    const uint32_t ks = s_ks[(base + u) * NB + tid];
-                    src = p.cur.pos + (int64_t)CHK(bucket_k(ks >> 3), p.grid.H) * LINE_WORDS + (ks & 7u);
-                }
-                sn[u] = xld(src);
-            }
+            if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
         }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
@@ -675,9 +653,6 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
         // dependent round trip per QB candidates, not one or two per bucket
         int k = 0, s = WIDE_HEAD_IDS;
         uint32_t tjn[QB];
-        // slot snapshots: the next batch's slot indices (bucket x 32 + slot)
-        // wait in the lane's LDS column past the buckets and counts
-        static_assert(16 + QB <= WIDE_MAXC, "rare path: slot indices fit the lane's column");
         auto load_ids = [&]() -> bool {           // the next batch's ids from cursor (k, s)
             bool any = false;
 #pragma unroll
@@ -685,9 +660,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 while (k < 8 && s >= (int32_t)s_cand[(8 + k) * NB + tid]) { ++k; s = WIDE_HEAD_IDS; }
                 tjn[u] = (uint32_t)i;
                 if (k < 8) {
-                    const uint32_t bk = s_cand[k * NB + tid];
-                    tjn[u] = xld(slot_word(p.cur, bk, s, rl));
-                    if (WIDE_SLOTPOS) s_cand[(16 + u) * NB + tid] = bk * (uint32_t)LINE_WORDS + (uint32_t)s;
+                    tjn[u] = xld(slot_word(p.cur, s_cand[k * NB + tid], s, rl));
                     ++s;
                     any = true;
                 }
@@ -701,15 +674,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
             for (int u = 0; u < QB; ++u) tj[u] = tjn[u];
             Snap<T> sn[QB];
-            if (WIDE_SLOTPOS && slotpos) {
-#pragma unroll
-                for (int u = 0; u < QB; ++u) {
-                    sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
-                    if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.cur.pos + s_cand[(16 + u) * NB + tid]);
-                }
-            } else {
-                gather(tj, sn);
-            }
+            gather(tj, sn);
             have = load_ids();
             test(tj, sn, 0, QB);
         }

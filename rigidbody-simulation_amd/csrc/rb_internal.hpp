@@ -60,13 +60,6 @@ template <typename T> struct Table {
     uint32_t *spill;           // ids past a full bucket: header (generation << 32 | count), then
                                // SPILL_CAP x {bucket, tagged id}; nullptr: none (an overflow is an error)
 };
-// The wide form reads candidates' positions from the table's slot
-// snapshots (Table::pos) where the world keeps them (rb_capi.hip
-// wide_slotpos; RBHIP_SLOTPOS=0: gathered by id from the snapshot)
-#ifndef RB_WIDE_SLOTPOS
-#define RB_WIDE_SLOTPOS 1
-#endif
-constexpr bool WIDE_SLOTPOS = RB_WIDE_SLOTPOS != 0;
 // A bucket holds 30 ids; a cell with more (a pile-up: C4's sliding rows
 // reach 29 by step 700) spills the rest into its table's spill list, which
 // a search reads only for a bucket whose count passed its slots.

@@ -158,11 +158,11 @@ template <typename T, int MAXP, bool BOXES, typename Overlap>
 __device__ __forceinline__ int32_t search_partners_wide(const StepParams<T> &p, int32_t i, int32_t kind, V3<T> x,
                                                         T rad, T bi, int32_t *s_id, uint32_t *s_cand, uint8_t *s_didx,
                                                         Snap<T> *s_hpos, int tid, uint32_t gen, bool &defer,
-                                                        Overlap overlap, uint8_t *s_ks = nullptr) {
+                                                        Overlap overlap) {
     return search_buckets_wide<T, MAXP>(
         p, i, x, s_id, s_cand, s_didx, s_hpos, tid, gen,
         [&](uint32_t tj, const Snap<T> &s) { return candidate_hit<T, BOXES>(p, i, kind, x, rad, bi, tj, s, defer); },
-        overlap, s_ks);
+        overlap);
 }
 
 // K1 for small scenes: G lanes per body, lane k of the group owns neighbour
@@ -561,7 +561,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
                                           int32_t *s_id, Snap<T> *s_pos, int32_t *t_id, Snap<T> *t_pos,
                                           uint32_t *s_cand, int32_t *cell, uint32_t gen, T *s_poly,
                                           uint8_t *s_didx = nullptr, Snap<T> *s_hpos = nullptr,
-                                          const T *s_help = nullptr, uint8_t *s_ks = nullptr) {
+                                          const T *s_help = nullptr) {
     constexpr int NB = STEP_BLOCK / G;
     const int32_t l = active ? (int32_t)lb : 0;
     const int32_t i = ld.lo + l;
@@ -611,7 +611,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
         // barriers, so the search runs under the active mask only
         if (RB_ABLATE != 1 && active)
             np_ = search_partners_wide<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, s_cand, s_didx, s_hpos, tid, gen,
-                                                       defer, [] {}, s_ks);
+                                                       defer, [] {});
         __syncthreads();                         // the search is done with s_cand: the helper fills it
         __syncthreads();
     } else if constexpr (G == 1 && WIDE) {
@@ -623,7 +623,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
                     apply_force(p, l, in.m, invI, in.v, in.w);
                     forced = true;
                 }
-            }, s_ks);
+            });
     } else if constexpr (G == 1) {
         if (RB_ABLATE != 1) np_ = search_partners<T, MAXP, BOXES>(p, i, kind, x, sz.x, bi, s_id, tid, gen, defer);
     } else if constexpr (HELP) {
@@ -811,7 +811,6 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     __shared__ T s_poly[BOXES ? 48 * NB : 1];   // box-box face clipping: 2 x 8 vertices x 3 per body
     __shared__ uint32_t s_cand[WIDE ? WIDE_MAXC * NB : 1];
     __shared__ uint8_t s_didx[WIDE ? MAXP * NB : 1];
-    __shared__ uint8_t s_ks[WIDE && WIDE_SLOTPOS ? WIDE_MAXC * NB : 1];   // candidates' (bucket, slot) in the heads
     __shared__ Snap<T> s_hpos[WIDE && RB_WIDE_LDSPOS ? WIDE_HPOS * NB : 1];
     __shared__ int32_t t_id[G > 1 ? MAXP * NB : 1];
     __shared__ Snap<T> s_pos[G > 1 ? MAXP * NB : 1];
@@ -850,8 +849,7 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
     int32_t cell[3] = {INT32_MAX, 0, 0};
     if (G > 1 || HELP || active)                 // (a helper's barriers: every lane)
         body_step<T, MAXP, G, WIDE, BOXES, true, HELP>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand,
-                                                       cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, help_lds,
-                                                       s_ks);
+                                                       cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, help_lds);
     if (p.bounds) fold_bounds(p.bounds, cell);
     if (blockIdx.x == 0 && tid == 0) {
         if (p.next.line) *p.next.gen = *p.cur.gen + 1u;

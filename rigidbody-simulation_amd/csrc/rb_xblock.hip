@@ -47,7 +47,6 @@
 #define RB_STEP_BLOCK 512        // (rb_internal.hpp XB_THREADS): the wide form's LDS columns
 #define RB_WIDE_LDSPOS 0         // partner snapshots re-read in the solve (L2-resident here)
 #define RB_WIDE_QBATCH 8         // candidates per round trip: two waves per SIMD must fit in 256 registers
-#define RB_WIDE_SLOTPOS 0        // the groups' tables keep no slot snapshots
 #define RB_INST 0                // none of rb_kernels.hip's own kernels
 #include "rb_kernels.hip"
 
