@@ -374,8 +374,13 @@ def main():
     else:
         cands, probes = [], {}
         # last resort: torch.distributed's all-gather per step (host-driven)
-        for tr, halo, blocks in (("p2p", True, False), ("p2p", False, False), ("p2p", False, True),
-                                 ("rccl", "auto", False), ("nccl", False, False)):
+        # (the sharded K-step blocks, validated but measured slower per step
+        # than the per-step kernels on one GPU, DESIGN §4.2 / §6: probed only
+        # with RBHIP_BENCH_BLOCKS=1)
+        modes = [("p2p", True, False), ("p2p", False, False)]
+        if os.environ.get("RBHIP_BENCH_BLOCKS") == "1":
+            modes.append(("p2p", False, True))
+        for tr, halo, blocks in modes + [("rccl", "auto", False), ("nccl", False, False)]:
             if tr in ("rccl", "nccl") and cands:
                 break
             try:
