@@ -593,6 +593,19 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     }
     int32_t np_ = 0, nh = 0;
     bool overflow = false;
+    // hits are appended in discovery order and ranked by id once the search
+    // is done (below): sorting each into place as it came cost a dependent
+    // LDS read per list entry passed — C4's pile-ups, up to 28 partners,
+    // spent ~40k cycles per step there
+    auto append = [&](int32_t j, const Snap<T> &sn) {
+        if (np_ >= MAXP) { overflow = true; return; }
+        s_id[np_ * NB + tid] = j;
+        if (RB_WIDE_LDSPOS) {
+            if (nh < WIDE_HPOS) s_hpos[nh * NB + tid] = sn;
+            ++nh;
+        }
+        ++np_;
+    };
     // candidates WIDE_QBATCH at a time; the first batch is issued by every
     // lane (padding = the body itself, which loads nothing): measured 2-7 %
     // faster at 32k-65k bodies than a loop all of whose batches are
@@ -610,8 +623,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
         for (int u = 0; u < QB; ++u)
             if (base + u < n && hit(tj[u], sn[u])) {
-                if (RB_WIDE_LDSPOS) list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u], overflow);
-                else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+                append((int32_t)(tj[u] & ~BOX_FLAG), sn[u]);
             }
     };
     batch(0);
@@ -631,10 +643,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
 #pragma unroll
             for (int u = 0; u < QB; ++u)
                 if (s0 + u < ck && hit(tj[u], sn[u])) {
-                    if (RB_WIDE_LDSPOS)
-                        list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)(tj[u] & ~BOX_FLAG), sn[u],
-                                              overflow);
-                    else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)(tj[u] & ~BOX_FLAG), overflow);
+                    append((int32_t)(tj[u] & ~BOX_FLAG), sn[u]);
                 }
         };
         auto gather = [&](const uint32_t (&tj)[QB], Snap<T> (&sn)[QB]) {
@@ -705,10 +714,26 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
                 if (j == (uint32_t)i) return;
                 const Snap<T> sn = xld(p.snap_cur + CHK(j, p.n_global));
                 if (!hit(t, sn)) return;
-                if (RB_WIDE_LDSPOS) list_insert_pos<MAXP>(s_id, s_didx, s_hpos, NB, tid, np_, nh, (int32_t)j, sn, overflow);
-                else list_insert<MAXP>(s_id, NB, tid, np_, (int32_t)j, overflow);
+                append((int32_t)j, sn);
             });
         }
+    }
+    // the partners in ascending id (the reference's contact order): each
+    // one's rank = how many are smaller (distinct ids: the wide search
+    // visits every bucket once, and a body sits in one bucket or the spill
+    // list), written to the lane's s_cand column, then back; s_didx maps a
+    // rank to the discovery index (the s_hpos slot)
+    if (np_ > 1) {
+        for (int u = 0; u < np_; ++u) {
+            const int32_t v = s_id[u * NB + tid];
+            int r = 0;
+            for (int q = 0; q < np_; ++q) r += s_id[q * NB + tid] < v ? 1 : 0;
+            s_cand[r * NB + tid] = (uint32_t)v;
+            if (RB_WIDE_LDSPOS) s_didx[r * NB + tid] = (uint8_t)u;
+        }
+        for (int u = 0; u < np_; ++u) s_id[u * NB + tid] = (int32_t)s_cand[u * NB + tid];
+    } else if (RB_WIDE_LDSPOS && np_ == 1) {
+        s_didx[tid] = 0;
     }
     STAMP(10);
     if (overflow) atomicOr(p.err, ERR_PARTNER_OVERFLOW);
