@@ -22,14 +22,16 @@ Scaling (body-id range shards, positions exchanged every step):
   weak              N patches of the config side by side on one shared
                     ground, one per rank (per-GPU work fixed).
 The ranks exchange positions inside the library, peer-to-peer over xGMI,
-in one of three modes: halo pushes (each step, each rank pushes to each
-peer only its bodies within a cell of the peer's bounds), full slice reads
-(each step), or sharded K-step blocks (every K steps each rank pushes the
-full state of its bodies within the blocks' ghost band of each peer, then
-steps own bodies plus ghosts K times in XCD-resident blocks).  All are
-warmed up, validated and timed over 20 steps on the node itself; the
-fastest valid one runs the timed region (`config.exchange_probe_ms_per_step`
-lists them).  RCCL is the fallback when none validates.
+in one of two modes: halo pushes (each step, each rank pushes to each
+peer only its bodies within a cell of the peer's bounds) or full slice
+reads (each step); with RBHIP_BENCH_BLOCKS=1 also sharded K-step blocks
+(every K steps each rank pushes the full state of its bodies within the
+blocks' ghost band of each peer, then steps own bodies plus ghosts K times
+in XCD-resident blocks: bit-exact, slower per step on MI355X).
+Each is warmed up, validated and timed over 20 steps on the node itself;
+the fastest valid one runs the timed region
+(`config.exchange_probe_ms_per_step` lists them).  RCCL is the fallback
+when none validates.
 
 N > 1 is validated: after the warmup and again after the timed region, every
 rank's bodies must be bit-identical (compared as uint64 words, so the sign
