@@ -723,14 +723,13 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     // visits every bucket once, and a body sits in one bucket or the spill
     // list), written to the lane's s_cand column, then back; s_didx maps a
     // rank to the discovery index (the s_hpos slot)
-    // (the rank loop's reads are unrolled over the list's capacity, so they
-    // issue back to back instead of one LDS round trip per entry)
+    // (the rank loop unrolled over the list's capacity measured slower:
+    // C4's pile-up 72.0 -> 87.7 us, profiles/r04/rank_unroll_ab_c4.log)
     if (np_ > 1) {
         for (int u = 0; u < np_; ++u) {
             const int32_t v = s_id[u * NB + tid];
             int r = 0;
-#pragma unroll
-            for (int q = 0; q < MAXP; ++q) r += (q < np_ && s_id[q * NB + tid] < v) ? 1 : 0;
+            for (int q = 0; q < np_; ++q) r += s_id[q * NB + tid] < v ? 1 : 0;
             s_cand[r * NB + tid] = (uint32_t)v;
             if (RB_WIDE_LDSPOS) s_didx[r * NB + tid] = (uint8_t)u;
         }
