@@ -543,6 +543,49 @@ template <int S> __device__ __forceinline__ uint32_t head6_id(const Head6 &h) {
 // fetched WIDE_QBATCH at a time.  Slots past 6 (rare: a bucket of 7+
 // bodies) are read afterwards, ids then snapshots.  overlap() runs under
 // the head loads.  Meant for one wave per SIMD: it holds many registers.
+// The lane's partner list (its s_id column, np entries, distinct) sorted
+// ascending in registers: padded to MAXP with INT32_MAX, a bitonic network
+// (MAXP = 16 or 32: 80 / 240 compare-exchanges, no memory round trip), then
+// written back; with s_didx, each sorted entry's discovery index among the
+// first WIDE_HPOS discovered (255 past them), from those ids kept aside.
+constexpr int WIDE_RANK_MAX = 8;                     // longer lists: the bitonic network
+template <int MAXP>
+__device__ __forceinline__ void sort_partners_bitonic(int32_t *s_id, uint8_t *s_didx, int stride, int slot, int32_t np,
+                                                      int32_t nh) {
+    static_assert(MAXP == 16 || MAXP == 32, "bitonic: a power of two");
+    int32_t a[MAXP];
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q) a[q] = q < np ? s_id[q * stride + slot] : INT32_MAX;
+    int32_t first[WIDE_HPOS];
+#pragma unroll
+    for (int q = 0; q < WIDE_HPOS; ++q) first[q] = q < nh ? a[q] : -1;
+#pragma unroll
+    for (int k = 2; k <= MAXP; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int q = 0; q < MAXP; ++q) {
+                const int l = q ^ j;
+                if (l > q) {
+                    const int32_t lo = min(a[q], a[l]), hi = max(a[q], a[l]);
+                    const bool up = (q & k) == 0;
+                    a[q] = up ? lo : hi;
+                    a[l] = up ? hi : lo;
+                }
+            }
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q)
+        if (q < np) {
+            s_id[q * stride + slot] = a[q];
+            if (s_didx) {
+                int d = 255;
+#pragma unroll
+                for (int f = 0; f < WIDE_HPOS; ++f) d = first[f] == a[q] ? f : d;
+                s_didx[q * stride + slot] = (uint8_t)d;
+            }
+        }
+}
+
 template <typename T, int MAXP, typename Hit, typename Overlap>
 __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, int32_t i, V3<T> x, int32_t *s_id,
                                                        uint32_t *s_cand, uint8_t *s_didx, Snap<T> *s_hpos, int tid,
@@ -718,14 +761,18 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
             });
         }
     }
-    // the partners in ascending id (the reference's contact order): each
-    // one's rank = how many are smaller (distinct ids: the wide search
-    // visits every bucket once, and a body sits in one bucket or the spill
-    // list), written to the lane's s_cand column, then back; s_didx maps a
-    // rank to the discovery index (the s_hpos slot)
-    // (the rank loop unrolled over the list's capacity measured slower:
-    // C4's pile-up 72.0 -> 87.7 us, profiles/r04/rank_unroll_ab_c4.log)
-    if (np_ > 1) {
+    // the partners in ascending id (the reference's contact order; distinct
+    // ids: the wide search visits every bucket once, and a body sits in one
+    // bucket or the spill list).  Long lists (C4's pile-ups, up to 28) are
+    // sorted in registers by a bitonic network; short ones by rank: each
+    // one's rank = how many are smaller, written to the lane's s_cand
+    // column, then back.  s_didx maps a sorted position to the discovery
+    // index (the s_hpos slot).  (The rank loop unrolled over the list's
+    // capacity measured slower: C4's pile-up 72.0 -> 87.7 us,
+    // profiles/r04/rank_unroll_ab_c4.log)
+    if (np_ > WIDE_RANK_MAX) {
+        sort_partners_bitonic<MAXP>(s_id, RB_WIDE_LDSPOS ? s_didx : nullptr, NB, tid, np_, nh);
+    } else if (np_ > 1) {
         for (int u = 0; u < np_; ++u) {
             const int32_t v = s_id[u * NB + tid];
             int r = 0;
