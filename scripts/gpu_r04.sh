@@ -48,6 +48,10 @@ for step in "$@"; do
               SIZES=256x256,128x256,256x32 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
               run rank_ab_c4 300 env "LIBS=build/ab_rank1.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
               SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
+        qbab) run qb_ab_c3 300 env "LIBS=build/ab_qb16.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=flat \
+              SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
+              run qb_ab_c4 300 env "LIBS=build/ab_qb16.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
+              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
         atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
