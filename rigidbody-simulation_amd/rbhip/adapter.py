@@ -204,9 +204,17 @@ def step_model(model, data, nsteps: int, dt: float, restitution: float, friction
         w.set_state(qpos[:7 * n].reshape(n, 7), qvel[:6 * n].reshape(n, 6))
     else:
         w.set_state(qpos[qi], qvel[vi])
-    xf = np.asarray(getattr(data, "xfrc_applied", np.zeros((1, 6))))
-    xf_free = xf[fb] if xf.shape[0] > fb[-1] else None
-    w.set_xfrc(xf_free if xf_free is not None and np.any(xf_free) else None)
+    # applied forces (collision.py:66-70): the common all-zero array is told
+    # by one contiguous scan, without gathering the free bodies' rows
+    xf = getattr(data, "xfrc_applied", None)
+    xf_free = None
+    if xf is not None:
+        xf = np.asarray(xf)
+        if xf.shape[0] > fb[-1] and xf.any():
+            xf_free = xf[fb]
+            if not np.any(xf_free):
+                xf_free = None
+    w.set_xfrc(xf_free)
     w.step(nsteps, dt=dt, restitution=restitution, friction=friction, threshold=threshold)
     if contiguous:
         w.get_state(data.qpos[:7 * n].reshape(n, 7), data.qvel[:6 * n].reshape(n, 6))
