@@ -289,6 +289,7 @@ struct rb_world {
     // while mirror_version == state_version (every change of the state bumps
     // it): an rb_set_state with exactly those bytes is then a no-op
     double *io_q_h = nullptr, *io_v_h = nullptr;   // pinned [N][7], [N][6]
+    hipEvent_t io_ev[4] = {};      // rb_get_state: the download in chunks, each copied out as it lands
     double *io_q_d = nullptr, *io_v_d = nullptr;   // device
     int64_t state_version = 0, mirror_version = -1;
     int64_t io_stats[2] = {};      // rb_set_state calls skipped (unchanged), uploads
@@ -1575,6 +1576,8 @@ void free_world(rb_world *w) {
     if (w->io_v_h) (void)hipHostFree(w->io_v_h);
     if (w->io_q_d) (void)hipFree(w->io_q_d);
     if (w->io_v_d) (void)hipFree(w->io_v_d);
+    for (hipEvent_t &e : w->io_ev)
+        if (e) (void)hipEventDestroy(e);
     void *bufs[] = {w->snap[0], w->snap[1], w->qsnap[0], w->qsnap[1], w->defer_q, w->defer_cnt, w->state, w->consts, w->kind, w->xfrc, w->gen,
                     w->ids[0], w->ids[1], w->spill[0], w->spill[1], w->pos[0], w->pos[1], w->plist, w->plist_cnt, w->vel[0], w->vel[1], w->err, w->rec_count, w->rec_partner, w->rec_kind,
                     w->rec_dist};
@@ -1933,13 +1936,26 @@ int rb_get_state(rb_world *w, double *qpos, double *qvel) {
     const hipError_t e = w->dtype == RB_F64 ? launch_state_out<double>(make_io<double>(w), qpos, qvel, w->stream)
                                             : launch_state_out<float>(make_io<float>(w), qpos, qvel, w->stream);
     HIPCHK(e);
-    // the owned rows only (a shard leaves the others untouched)
+    // the owned rows only (a shard leaves the others untouched), in up to
+    // four chunks: each chunk is copied out to the caller while the later
+    // ones are still crossing PCIe
     const size_t lo = (size_t)w->lo, n = (size_t)w->n_local;
-    if (qpos) HIPCHK(hipMemcpyAsync(w->io_q_h + 7 * lo, w->io_q_d + 7 * lo, sizeof(double) * 7 * n, hipMemcpyDeviceToHost, w->stream));
-    if (qvel) HIPCHK(hipMemcpyAsync(w->io_v_h + 6 * lo, w->io_v_d + 6 * lo, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, w->stream));
-    HIPCHK(hipStreamSynchronize(w->stream));
-    if (qpos) par_copy(qpos + 7 * lo, w->io_q_h + 7 * lo, 7 * n);
-    if (qvel) par_copy(qvel + 6 * lo, w->io_v_h + 6 * lo, 6 * n);
+    const int nc = n >= 16384 ? 4 : 1;
+    if (nc > 1 && !w->io_ev[0])
+        for (hipEvent_t &e : w->io_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int c = 0; c < nc; ++c) {
+        const size_t a = lo + n * c / nc, b = lo + n * (c + 1) / nc;
+        if (qpos) HIPCHK(hipMemcpyAsync(w->io_q_h + 7 * a, w->io_q_d + 7 * a, sizeof(double) * 7 * (b - a), hipMemcpyDeviceToHost, w->stream));
+        if (qvel) HIPCHK(hipMemcpyAsync(w->io_v_h + 6 * a, w->io_v_d + 6 * a, sizeof(double) * 6 * (b - a), hipMemcpyDeviceToHost, w->stream));
+        if (nc > 1) HIPCHK(hipEventRecord(w->io_ev[c], w->stream));
+    }
+    for (int c = 0; c < nc; ++c) {
+        const size_t a = lo + n * c / nc, b = lo + n * (c + 1) / nc;
+        if (nc > 1) HIPCHK(hipEventSynchronize(w->io_ev[c]));
+        else HIPCHK(hipStreamSynchronize(w->stream));
+        if (qpos) par_copy(qpos + 7 * a, w->io_q_h + 7 * a, 7 * (b - a));
+        if (qvel) par_copy(qvel + 6 * a, w->io_v_h + 6 * a, 6 * (b - a));
+    }
     w->mirror_version = (w->P == 1 && qpos && qvel) ? w->state_version : -1;
     return RB_OK;
 }
