@@ -289,7 +289,8 @@ struct rb_world {
     // while mirror_version == state_version (every change of the state bumps
     // it): an rb_set_state with exactly those bytes is then a no-op
     double *io_q_h = nullptr, *io_v_h = nullptr;   // pinned [N][7], [N][6]
-    hipEvent_t io_ev[4] = {};      // rb_get_state: the download in chunks, each copied out as it lands
+    double *io_q_hd = nullptr, *io_v_hd = nullptr; // the same pinned rows, device-mapped (rb_get_state's kernel writes them)
+    hipEvent_t io_ev[4] = {};      // rb_get_state (RBHIP_IO_OUT=1): the download in chunks, each copied out as it lands
     double *io_q_d = nullptr, *io_v_d = nullptr;   // device
     int64_t state_version = 0, mirror_version = -1;
     int64_t io_stats[2] = {};      // rb_set_state calls skipped (unchanged), uploads
@@ -1487,12 +1488,25 @@ class HostPool {
         done_cv_.wait(lk, [&] { return done_.load() == pieces_ && busy_ == 0; });
     }
 };
-void par_copy(double *dst, const double *src, size_t n) {
-    HostPool::get().run(n, [&](size_t lo, size_t hi) { memcpy(dst + lo, src + lo, sizeof(double) * (hi - lo)); });
+// fn(array, lo, hi) over [0, n0) of array 0 and [0, n1) of array 1, in one
+// pool run (one wake-up of the workers for both of a state's arrays)
+template <typename F> void par_two(size_t n0, size_t n1, const F &fn) {
+    HostPool::get().run(n0 + n1, [&](size_t lo, size_t hi) {
+        if (lo < n0) fn(0, lo, std::min(hi, n0));
+        if (hi > n0) fn(1, std::max(lo, n0) - n0, hi - n0);
+    });
 }
-bool par_equal(const double *a, const double *b, size_t n) {
+// dst_k[0, n_k) = src_k[0, n_k), k = 0, 1
+void par_copy2(double *d0, const double *s0, size_t n0, double *d1, const double *s1, size_t n1) {
+    par_two(n0, n1, [&](int k, size_t lo, size_t hi) {
+        if (k == 0) memcpy(d0 + lo, s0 + lo, sizeof(double) * (hi - lo));
+        else memcpy(d1 + lo, s1 + lo, sizeof(double) * (hi - lo));
+    });
+}
+bool par_equal2(const double *a0, const double *b0, size_t n0, const double *a1, const double *b1, size_t n1) {
     std::atomic<int> diff{0};
-    HostPool::get().run(n, [&](size_t lo, size_t hi) {
+    par_two(n0, n1, [&](int k, size_t lo, size_t hi) {
+        const double *a = k ? a1 : a0, *b = k ? b1 : b0;
         if (!diff.load(std::memory_order_relaxed) && memcmp(a + lo, b + lo, sizeof(double) * (hi - lo)) != 0) diff = 1;
     });
     return diff.load() == 0;
@@ -1501,8 +1515,12 @@ bool par_equal(const double *a, const double *b, size_t n) {
 int io_alloc(rb_world *w) {
     if (w->io_q_h) return RB_OK;
     const size_t nq = (size_t)7 * w->N, nv = (size_t)6 * w->N;
-    HIPCHK(hipHostMalloc((void **)&w->io_q_h, sizeof(double) * nq, 0));
-    HIPCHK(hipHostMalloc((void **)&w->io_v_h, sizeof(double) * nv, 0));
+    // mapped and coherent: rb_get_state's kernel stores into them across
+    // PCIe, visible to the host once the stream is synchronised
+    HIPCHK(hipHostMalloc((void **)&w->io_q_h, sizeof(double) * nq, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc((void **)&w->io_v_h, sizeof(double) * nv, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&w->io_q_hd, w->io_q_h, 0));
+    HIPCHK(hipHostGetDevicePointer((void **)&w->io_v_hd, w->io_v_h, 0));
     HIPCHK(hipMalloc((void **)&w->io_q_d, sizeof(double) * nq));
     HIPCHK(hipMalloc((void **)&w->io_v_d, sizeof(double) * nv));
     return RB_OK;
@@ -1904,15 +1922,13 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     // the state the last rb_get_state handed out, handed back unchanged (a
     // per-frame caller: multi_sphere_bounce.py:42 once per frame): nothing
     // to do (one rank: a shard's rows of other ranks are not mirrored)
-    if (w->P == 1 && w->mirror_version == w->state_version && par_equal(qpos, w->io_q_h, nq) &&
-        par_equal(qvel, w->io_v_h, nv)) {
+    if (w->P == 1 && w->mirror_version == w->state_version && par_equal2(qpos, w->io_q_h, nq, qvel, w->io_v_h, nv)) {
         w->io_stats[0] += 1;
         return RB_OK;
     }
     w->io_stats[1] += 1;
     HIPCHK(hipStreamSynchronize(w->stream));     // (a DMA out of the staging may be in flight)
-    par_copy(w->io_q_h, qpos, nq);
-    par_copy(w->io_v_h, qvel, nv);
+    par_copy2(w->io_q_h, qpos, nq, w->io_v_h, qvel, nv);
     fit_period(w, qpos);
     w->xb_cut_valid = false;                             // block slabs: refitted at the next block run
     HIPCHK(hipMemcpyAsync(w->io_q_d, w->io_q_h, sizeof(double) * nq, hipMemcpyHostToDevice, w->stream));
@@ -1933,28 +1949,44 @@ int rb_get_state(rb_world *w, double *qpos, double *qvel) {
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     if (int rc = io_alloc(w)) return rc;
-    const hipError_t e = w->dtype == RB_F64 ? launch_state_out<double>(make_io<double>(w), qpos, qvel, w->stream)
-                                            : launch_state_out<float>(make_io<float>(w), qpos, qvel, w->stream);
-    HIPCHK(e);
-    // the owned rows only (a shard leaves the others untouched), in up to
-    // four chunks: each chunk is copied out to the caller while the later
-    // ones are still crossing PCIe
+    // the owned rows only (a shard leaves the others untouched).
+    // RBHIP_IO_OUT=0: a kernel transposes into the device twin, one DMA, one
+    // pool copy out to the caller; =1 (default): the DMA in four chunks, each
+    // copied out as it lands; =2: the kernel stores the rows straight into
+    // the mapped pinned staging (no DMA), then one pool copy
+    const char *ev = getenv("RBHIP_IO_OUT");
+    const int mode = ev ? atoi(ev) : 1;
     const size_t lo = (size_t)w->lo, n = (size_t)w->n_local;
-    const int nc = n >= 16384 ? 4 : 1;
-    if (nc > 1 && !w->io_ev[0])
-        for (hipEvent_t &e : w->io_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (int c = 0; c < nc; ++c) {
-        const size_t a = lo + n * c / nc, b = lo + n * (c + 1) / nc;
-        if (qpos) HIPCHK(hipMemcpyAsync(w->io_q_h + 7 * a, w->io_q_d + 7 * a, sizeof(double) * 7 * (b - a), hipMemcpyDeviceToHost, w->stream));
-        if (qvel) HIPCHK(hipMemcpyAsync(w->io_v_h + 6 * a, w->io_v_d + 6 * a, sizeof(double) * 6 * (b - a), hipMemcpyDeviceToHost, w->stream));
-        if (nc > 1) HIPCHK(hipEventRecord(w->io_ev[c], w->stream));
-    }
-    for (int c = 0; c < nc; ++c) {
-        const size_t a = lo + n * c / nc, b = lo + n * (c + 1) / nc;
-        if (nc > 1) HIPCHK(hipEventSynchronize(w->io_ev[c]));
-        else HIPCHK(hipStreamSynchronize(w->stream));
-        if (qpos) par_copy(qpos + 7 * a, w->io_q_h + 7 * a, 7 * (b - a));
-        if (qvel) par_copy(qvel + 6 * a, w->io_v_h + 6 * a, 6 * (b - a));
+    const size_t nq = qpos ? 7 * n : 0, nv = qvel ? 6 * n : 0;
+    if (mode == 2) {
+        StateIO<double> pd = make_io<double>(w);
+        StateIO<float> pf = make_io<float>(w);
+        pd.qpos = pf.qpos = w->io_q_hd;
+        pd.qvel = pf.qvel = w->io_v_hd;
+        HIPCHK(w->dtype == RB_F64 ? launch_state_out_flat<double>(pd, qpos, qvel, w->stream)
+                                  : launch_state_out_flat<float>(pf, qpos, qvel, w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        par_copy2(qpos ? qpos + 7 * lo : nullptr, w->io_q_h + 7 * lo, nq, qvel ? qvel + 6 * lo : nullptr,
+                  w->io_v_h + 6 * lo, nv);
+    } else {
+        HIPCHK(w->dtype == RB_F64 ? launch_state_out<double>(make_io<double>(w), qpos, qvel, w->stream)
+                                  : launch_state_out<float>(make_io<float>(w), qpos, qvel, w->stream));
+        const int nc = mode == 1 && n >= 16384 ? 4 : 1;
+        if (nc > 1 && !w->io_ev[0])
+            for (hipEvent_t &e : w->io_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (int c = 0; c < nc; ++c) {
+            const size_t a = lo + n * c / nc, b = lo + n * (c + 1) / nc;
+            if (qpos) HIPCHK(hipMemcpyAsync(w->io_q_h + 7 * a, w->io_q_d + 7 * a, sizeof(double) * 7 * (b - a), hipMemcpyDeviceToHost, w->stream));
+            if (qvel) HIPCHK(hipMemcpyAsync(w->io_v_h + 6 * a, w->io_v_d + 6 * a, sizeof(double) * 6 * (b - a), hipMemcpyDeviceToHost, w->stream));
+            if (nc > 1) HIPCHK(hipEventRecord(w->io_ev[c], w->stream));
+        }
+        for (int c = 0; c < nc; ++c) {
+            const size_t a = lo + n * c / nc, b = lo + n * (c + 1) / nc;
+            if (nc > 1) HIPCHK(hipEventSynchronize(w->io_ev[c]));
+            else HIPCHK(hipStreamSynchronize(w->stream));
+            par_copy2(qpos ? qpos + 7 * a : nullptr, w->io_q_h + 7 * a, qpos ? 7 * (b - a) : 0,
+                      qvel ? qvel + 6 * a : nullptr, w->io_v_h + 6 * a, qvel ? 6 * (b - a) : 0);
+        }
     }
     w->mirror_version = (w->P == 1 && qpos && qvel) ? w->state_version : -1;
     return RB_OK;

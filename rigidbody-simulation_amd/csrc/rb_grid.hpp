@@ -672,6 +672,57 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
     batch(0);
     for (int base = QB; base < n; base += QB) batch(base);
     STAMP(9);
+#if RB_WIDE_PIPE == 2
+    if (RB_WIDE_MORE && more) {
+        // buckets of 7+ bodies, software-pipelined and batched across
+        // buckets as below, with the cursor in registers: the ids past the
+        // heads numbered 0..E[7]-1 bucket after bucket (E: running sums of
+        // the buckets' extra ids), and id t's bucket and slot selected from
+        // E and b by compares — a batch's QB id loads issue together, with
+        // no dependent LDS read per id
+        int32_t E[8];
+        int32_t e = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            e += c[k] > WIDE_HEAD_IDS ? c[k] - WIDE_HEAD_IDS : 0;
+            E[k] = e;
+        }
+        uint32_t tjn[QB];
+        auto load_ids = [&](int32_t t0) {
+#pragma unroll
+            for (int u = 0; u < QB; ++u) {
+                const int32_t t = t0 + u;
+                uint32_t bk = b[7];
+                int32_t base = E[6];
+#pragma unroll
+                for (int k = 6; k >= 0; --k)
+                    if (t < E[k]) { bk = b[k]; base = k ? E[k - 1] : 0; }
+                tjn[u] = t < e ? xld(slot_word(p.cur, bk, t - base + WIDE_HEAD_IDS, rl)) : (uint32_t)i;
+            }
+        };
+        load_ids(0);
+#pragma unroll 1
+        for (int32_t t0 = 0; t0 < e; t0 += QB) {
+            uint32_t tj[QB];
+#pragma unroll
+            for (int u = 0; u < QB; ++u) tj[u] = tjn[u];
+            Snap<T> sn[QB];
+#pragma unroll
+            for (int u = 0; u < QB; ++u) {
+                sn[u] = Snap<T>{x.x, x.y, x.z, T(0)};
+                if ((tj[u] & ~BOX_FLAG) != (uint32_t)i) sn[u] = xld(p.snap_cur + CHK(tj[u] & ~BOX_FLAG, p.n_global));
+            }
+            if (t0 + QB < e) load_ids(t0 + QB);
+#pragma unroll
+            for (int u = 0; u < QB; ++u)
+                if (t0 + u < e && hit(tj[u], sn[u])) append((int32_t)(tj[u] & ~BOX_FLAG), sn[u]);
+        }
+    }
+    if (RB_WIDE_MORE && spm) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s_cand[k * NB + tid] = b[k];
+    }
+#else
     if (RB_WIDE_MORE && more) {
         // buckets of 7+ bodies: the remaining ids from their lines, QB at a
         // time.  Rare, so kept compact: the buckets and counts go to the
@@ -748,6 +799,7 @@ __device__ __forceinline__ int32_t search_buckets_wide(const StepParams<T> &p, i
         }
 #endif
     }
+#endif
     if (RB_WIDE_MORE && spm) {                        // rarer: ids past full buckets (a spilled
 #pragma unroll 1                                      // bucket is a 7+ one: its index is stashed)
         for (int k = 0; k < 8; ++k) {

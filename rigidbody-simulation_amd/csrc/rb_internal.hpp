@@ -414,6 +414,7 @@ template <typename T> struct StateIO {
 };
 template <typename T> hipError_t launch_state_in(const StateIO<T> &p, hipStream_t s);
 template <typename T> hipError_t launch_state_out(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s);
+template <typename T> hipError_t launch_state_out_flat(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);

@@ -341,6 +341,11 @@ template <typename T> struct Lead {
 #ifndef RB_SOLVE_PIPE
 #define RB_SOLVE_PIPE 1
 #endif
+// the wide sphere kernels: each partner batch's contact geometry computed
+// first, then its solves branch-free (impulse_apply_sel), in one basic block
+#ifndef RB_SOLVE_FLAT
+#define RB_SOLVE_FLAT 0
+#endif
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 template <typename T>
@@ -453,6 +458,38 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             if (s0 + PB < np_) fetch(s0 + PB, jn, sn_next);
         } else {
             fetch(s0, jj, pe);
+        }
+        if constexpr (!BOXES && RB_SOLVE_FLAT && PM == 2) {
+            // the batch's geometry (step-start data only), then its
+            // sequential solves; padding entries solve nothing
+            Contact<T> cn[PB];
+            V3<T> nn[PB];
+#pragma unroll
+            for (int u = 0; u < PB; ++u)
+                if (s0 + u >= np_) {                         // (fetch leaves them unset)
+                    jj[u] = i;
+                    pe[u] = Snap<T>{x.x + T(1), x.y, x.z, sz.x};
+                }
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {
+                const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};
+                const bool lo = i < jj[u];                   // this body is geom1
+                sphere_sphere(lo ? x : cj, lo ? sz.x : pe[u].r, lo ? cj : x, lo ? pe[u].r : sz.x, cn[u]);
+                nn[u] = (lo && p.oriented) ? V3<T>{-cn[u].frame.x, -cn[u].frame.y, -cn[u].frame.z} : cn[u].frame;
+            }
+            if (p.rec_count) {
+#pragma unroll
+                for (int u = 0; u < PB; ++u)
+                    if (s0 + u < np_) record(p, l, nrec, jj[u], 16, cn[u].dist);
+            }
+            const M3<T> &iI = invI.get();
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {
+                const bool live = s0 + u < np_ && cn[u].dist < T(0) && !(absval(cn[u].dist) < p.thr);
+                const V3<T> r = {cn[u].pos.x - x.x, cn[u].pos.y - x.y, cn[u].pos.z - x.z};
+                impulse_apply_sel(live, k, m, iI, r, nn[u], p.e, p.mu, v, w);
+            }
+            continue;
         }
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
@@ -1191,6 +1228,30 @@ __global__ __launch_bounds__(256) void state_out_kernel(StateIO<T> p, int want_q
     }
 }
 
+// The same rows written straight into mapped pinned host memory (p.qpos /
+// p.qvel host-mapped): one lane per output double, so every wave's store is
+// one contiguous 512 B run across PCIe (a lane per body would scatter 56 B
+// strides); the SoA rows are gathered from HBM instead.
+template <typename T>
+__global__ __launch_bounds__(256) void state_out_flat_kernel(StateIO<T> p, int want_q, int want_v) {
+    const int64_t nq = want_q ? 7 * (int64_t)p.n_local : 0, nv = want_v ? 6 * (int64_t)p.n_local : 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nq + nv; e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < nq) {
+            const int64_t l = e / 7;
+            const int d = (int)(e - 7 * l);
+            T x;
+            if (d >= 3) x = p.st.row(d - 3)[l];
+            else if (p.balls) x = p.st.row(10 + d)[l];
+            else x = reinterpret_cast<const T *>(p.snap + p.lo + l)[d];
+            p.qpos[7 * p.lo + e] = (double)x;
+        } else {
+            const int64_t f = e - nq, l = f / 6;
+            const int d = (int)(f - 6 * l);
+            p.qvel[6 * p.lo + f] = (double)p.st.row(4 + d)[l];
+        }
+    }
+}
+
 template <typename T> hipError_t launch_state_in(const StateIO<T> &p, hipStream_t s) {
     if (p.N <= 0) return hipSuccess;
     hipLaunchKernelGGL((state_in_kernel<T>), dim3((unsigned)((p.N + 255) / 256)), dim3(256), 0, s, p);
@@ -1200,6 +1261,13 @@ template <typename T> hipError_t launch_state_out(const StateIO<T> &p, bool want
     if (p.n_local <= 0) return hipSuccess;
     hipLaunchKernelGGL((state_out_kernel<T>), dim3((unsigned)((p.n_local + 255) / 256)), dim3(256), 0, s, p,
                        want_q ? 1 : 0, want_v ? 1 : 0);
+    return hipGetLastError();
+}
+template <typename T> hipError_t launch_state_out_flat(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s) {
+    if (p.n_local <= 0) return hipSuccess;
+    const int64_t n = 13 * (int64_t)p.n_local;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL((state_out_flat_kernel<T>), dim3(blocks), dim3(256), 0, s, p, want_q ? 1 : 0, want_v ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -1269,6 +1337,7 @@ template hipError_t launch_kat_narrow<double>(int64_t, const double *, double *,
 template hipError_t launch_insert<double>(const InsertParams<double> &, hipStream_t);
 template hipError_t launch_state_in<double>(const StateIO<double> &, hipStream_t);
 template hipError_t launch_state_out<double>(const StateIO<double> &, bool, bool, hipStream_t);
+template hipError_t launch_state_out_flat<double>(const StateIO<double> &, bool, bool, hipStream_t);
 template hipError_t launch_kat_impulse<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<double>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<double>(int64_t, const double *, double *, hipStream_t);
@@ -1279,6 +1348,7 @@ template hipError_t launch_kat_narrow<float>(int64_t, const double *, double *, 
 template hipError_t launch_insert<float>(const InsertParams<float> &, hipStream_t);
 template hipError_t launch_state_in<float>(const StateIO<float> &, hipStream_t);
 template hipError_t launch_state_out<float>(const StateIO<float> &, bool, bool, hipStream_t);
+template hipError_t launch_state_out_flat<float>(const StateIO<float> &, bool, bool, hipStream_t);
 template hipError_t launch_kat_impulse<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_inertia<float>(int64_t, const double *, double *, hipStream_t);
 template hipError_t launch_kat_apply<float>(int64_t, const double *, double *, hipStream_t);

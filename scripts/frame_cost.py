@@ -58,6 +58,31 @@ def frame_cost(cfg: str, frames: int):
     print(json.dumps({"what": "per-frame host cost (adapter.step_model, 1 step per call)", "config": cfg,
                       "bodies": sc.n, "frames": frames, "ms_per_call_median": 1e3 * float(np.median(tot)),
                       **{f"{k}_ms_median": 1e3 * float(np.median(v)) for k, v in parts.items()}}), flush=True)
+    # rb_get_state's download forms (RBHIP_IO_OUT, read per call), into the
+    # caller's existing arrays as step_model does: 0 one DMA, 1 the DMA in
+    # four chunks, 2 (default) the kernel storing into mapped pinned memory
+    qd, vd = np.zeros((sc.n, 7)), np.zeros((sc.n, 6))
+    for mode in ("0", "1", "2"):
+        os.environ["RBHIP_IO_OUT"] = mode
+        g, c = [], []
+        for _ in range(frames):
+            qd[:] = -1.0
+            w.step(1, **p)
+            w.sync()
+            t, _ = timed(lambda: w.get_state(qd, vd)); g.append(t)
+            t, _ = timed(lambda: adapter.step_model(model, data, 1, **p)); c.append(t)
+        print(json.dumps({"what": "rb_get_state download form", "RBHIP_IO_OUT": int(mode),
+                          "get_state_ms_median": 1e3 * float(np.median(g)),
+                          "step_model_ms_median": 1e3 * float(np.median(c))}), flush=True)
+    os.environ.pop("RBHIP_IO_OUT")
+    # the three forms hand out the same bytes
+    outs = []
+    for mode in ("0", "1", "2"):
+        os.environ["RBHIP_IO_OUT"] = mode
+        outs.append(w.get_state())
+    os.environ.pop("RBHIP_IO_OUT")
+    assert all(np.array_equal(o[0].view(np.uint64), outs[0][0].view(np.uint64)) and
+               np.array_equal(o[1].view(np.uint64), outs[0][1].view(np.uint64)) for o in outs)
 
 
 def window_times(sc, windows, **kw):

@@ -52,11 +52,20 @@ for step in "$@"; do
               SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
               run qb_ab_c4 300 env "LIBS=build/ab_qb16.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
               SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
+        rareab) run rare2_tests 600 env RBHIP_LIB_PATH=build/ab_rare2.so python -u -m pytest tests/test_gpu_parity.py -x -q \
+              -k "crowded or c4_2000 or past_the_head or contact_rich or c3_bench_windows" --timeout 300 --timeout-method thread &&
+              run flat_tests 600 env RBHIP_LIB_PATH=build/ab_flat.so python -u -m pytest tests/test_gpu_parity.py -x -q \
+              -k "crowded or c4_2000 or past_the_head or contact_rich or c3_bench_windows or xfrc or f32_bit" --timeout 300 --timeout-method thread &&
+              run solve_ab_c4 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_rare2.so;build/ab_flat.so" SCENE=incline \
+              SIZES=256x256 WARM=500 ROUNDS=3 python -u scripts/ablate.py &&
+              run solve_ab_c3 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_rare2.so;build/ab_flat.so" SCENE=flat \
+              SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py ;;
         atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
         stampsc4) run stamps_c4 300 python -u scripts/stamps_c4.py --warm 700 ;;
         framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
+        framecostq) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 --skip-drift ;;
         pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ;;
         benchK) run bench_k400 300 python -u bench.py --steps 400 --warmup 5 ;;
