@@ -210,7 +210,7 @@ def step_model(model, data, nsteps: int, dt: float, restitution: float, friction
     xf_free = None
     if xf is not None:
         xf = np.asarray(xf)
-        if xf.shape[0] > fb[-1] and xf.any():
+        if xf.shape[0] > fb[-1] and not _all_zero(xf):
             xf_free = xf[fb]
             if not np.any(xf_free):
                 xf_free = None
@@ -222,6 +222,16 @@ def step_model(model, data, nsteps: int, dt: float, restitution: float, friction
         q, v = w.get_state()
         data.qpos[qi] = q
         data.qvel[vi] = v
+
+
+def _all_zero(a: np.ndarray) -> bool:
+    """not a.any(), fast for the common all-+0.0 float64 array: the largest
+    64-bit word is 0 only then (one integer max, ~10x faster than any() on
+    65,537 x 6); anything else (a -0.0, a force) decided by any()."""
+    if a.dtype == np.float64 and a.flags.c_contiguous and a.size:
+        if int(a.reshape(-1).view(np.uint64).max()) == 0:
+            return True
+    return not a.any()
 
 
 def _layout(model, w: World):

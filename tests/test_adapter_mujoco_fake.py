@@ -129,3 +129,23 @@ def test_step_model_writes_free_joints_only(fake_mujoco, monkeypatch):
     assert d.qpos[0] == q0[0] and d.qvel[0] == v0[0]
     assert np.array_equal(d.qpos[1:], q0[1:] + 1.0) and np.array_equal(d.qvel[1:], v0[1:] + 1.0)
     assert seen["xf"] is None
+
+
+def test_all_zero_applied_forces_check():
+    """step_model's per-frame all-zero test of xfrc_applied (the integer-max
+    fast path) decides exactly as `not a.any()`: -0.0 is zero, a denormal,
+    a NaN or a force in a strided view is not."""
+    sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "..",
+                                                  "rigidbody-simulation_amd"))
+    from rbhip.adapter import _all_zero
+    rng = np.random.default_rng(3)
+    cases = [np.zeros((65, 6)), np.zeros((0, 6)), np.zeros((9, 12))[:, :6], np.zeros((5, 6), np.float32)]
+    for v in (-0.0, 5e-324, np.nan, np.inf, -1.0, 1e300):
+        a = np.zeros((65, 6))
+        a[rng.integers(65), rng.integers(6)] = v
+        cases.append(a)
+    b = np.zeros((9, 12))
+    b[4, 3] = 2.0
+    cases += [b[:, :6], b[:, 6:]]
+    for a in cases:
+        assert _all_zero(a) == (not a.any())
