@@ -1462,7 +1462,7 @@ class HostPool {
         int want = 8;
         if (const char *ev = getenv("OMP_NUM_THREADS")) want = atoi(ev);
         if (const char *ev = getenv("RBHIP_HOST_THREADS")) want = atoi(ev);
-        want = std::max(1, std::min(want, 8));
+        want = std::max(1, std::min(want, 16));
         for (int k = 1; k < want; ++k) th_.emplace_back([this] { loop(); });
     }
     ~HostPool() {

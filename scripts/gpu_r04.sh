@@ -66,6 +66,7 @@ for step in "$@"; do
         stampsc4) run stamps_c4 300 python -u scripts/stamps_c4.py --warm 700 ;;
         framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
         framecostq) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 --skip-drift ;;
+        framecost8) run frame_cost_t8 300 env RBHIP_HOST_THREADS=8 python -u scripts/frame_cost.py --config c3 --frames 20 --skip-drift ;;
         pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ;;
         benchK) run bench_k400 300 python -u bench.py --steps 400 --warmup 5 ;;

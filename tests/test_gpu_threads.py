@@ -75,3 +75,35 @@ def test_unchanged_set_state_is_a_no_op_and_exact(rb_lib=None):
         assert np.array_equal(v.view(np.uint64), v_ref.view(np.uint64))
         st = w.stats()
         assert st["io_skipped"] >= 25 and st["io_uploads"] >= 2, st
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_get_state_download_forms_agree(monkeypatch, dtype):
+    """rb_get_state's three download forms (RBHIP_IO_OUT, read per call:
+    0 one DMA, 1 the DMA in four chunks — taken from 16,384 bodies — and 2
+    the kernel storing into mapped pinned memory) hand out the same bytes,
+    into fresh and into caller-owned arrays, and each leaves the staging a
+    mirror of the state (the next unchanged rb_set_state is skipped)."""
+    import rbhip
+    from rbhip import scenes
+    rbhip.load()
+    sc = scenes.flat_spheres(160, 128, seed=5)          # 20,480 bodies: the chunked form splits
+    with rbhip.World(sc, dtype=dtype) as w:
+        w.set_state(sc.qpos0, sc.qvel0)
+        w.step(7)
+        outs = []
+        for mode in ("0", "1", "2"):
+            monkeypatch.setenv("RBHIP_IO_OUT", mode)
+            q, v = w.get_state()
+            qd, vd = np.full((sc.n, 7), -7.0), np.full((sc.n, 6), -7.0)
+            w.get_state(qd, vd)
+            assert np.array_equal(q.view(np.uint64), qd.view(np.uint64))
+            assert np.array_equal(v.view(np.uint64), vd.view(np.uint64))
+            before = w.stats()["io_skipped"]
+            w.set_state(q, v)
+            assert w.stats()["io_skipped"] == before + 1, mode
+            outs.append((q, v))
+        for q, v in outs[1:]:
+            assert np.array_equal(q.view(np.uint64), outs[0][0].view(np.uint64))
+            assert np.array_equal(v.view(np.uint64), outs[0][1].view(np.uint64))
+        assert np.isfinite(outs[0][0]).all() and (outs[0][0][:, 3:] != 0).any()
