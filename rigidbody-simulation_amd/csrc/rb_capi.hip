@@ -1949,13 +1949,15 @@ int rb_get_state(rb_world *w, double *qpos, double *qvel) {
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     if (int rc = io_alloc(w)) return rc;
-    // the owned rows only (a shard leaves the others untouched).
-    // RBHIP_IO_OUT=0: a kernel transposes into the device twin, one DMA, one
-    // pool copy out to the caller; =1 (default): the DMA in four chunks, each
-    // copied out as it lands; =2: the kernel stores the rows straight into
-    // the mapped pinned staging (no DMA), then one pool copy
+    // the owned rows only (a shard leaves the others untouched).  Default
+    // (RBHIP_IO_OUT=2): one kernel stores the rows straight into the mapped
+    // pinned staging (no DMA), then one pool copy out to the caller.  =0: a
+    // kernel transposes into the device twin, one DMA, one pool copy; =1:
+    // that DMA in four chunks, each copied out as it lands.  65,536 bodies
+    // into the caller's arrays, MI355X: 0.21 / 0.22 / 0.28 ms for 2 / 0 / 1
+    // (profiles/r04/frame_cost_16threads.log)
     const char *ev = getenv("RBHIP_IO_OUT");
-    const int mode = ev ? atoi(ev) : 1;
+    const int mode = ev ? atoi(ev) : 2;
     const size_t lo = (size_t)w->lo, n = (size_t)w->n_local;
     const size_t nq = qpos ? 7 * n : 0, nv = qvel ? 6 * n : 0;
     if (mode == 2) {

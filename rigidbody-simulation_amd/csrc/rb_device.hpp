@@ -166,32 +166,6 @@ __device__ __forceinline__ void apply(V3<T>& v, V3<T>& w, T m, const M3<T>& invI
     w = {w.x + dw.x, w.y + dw.y, w.z + dw.z};
 }
 
-// impulse() then apply() without branches: every value is computed and the
-// update selected (the same bits as the branching pair: a skipped contact
-// leaves v, w as they were).  `live` = the caller's skip rules passed; the
-// contact then applies iff !(u_rel_n >= 0), as impulse() decides.  Straight
-// -line, so a partner batch's contacts share one basic block and the
-// scheduler can overlap the next contact's geometry with this chain.
-template <typename T>
-__device__ __forceinline__ void impulse_apply_sel(bool live, T k, T m, const M3<T>& invI, V3<T> r, V3<T> n, T e, T mu,
-                                                  V3<T>& v, V3<T>& w) {
-    const V3<T> c = np_cross(w, r);
-    const V3<T> u = {v.x + c.x, v.y + c.y, v.z + c.z};
-    const T un = np_dot(u, n);
-    const V3<T> ut = {u.x - un * n.x, u.y - un * n.y, u.z - un * n.z};
-    const T jn = (-(T(1) + e) * un) / k;
-    const T nut = sqroot(np_dot(ut, ut));
-    const T mf = mu * absval(jn);
-    const T s = -((nut < mf) ? nut : mf);
-    const bool fr = nut > T(1e-6);
-    const V3<T> jt = {fr ? s * (ut.x / nut) : T(0), fr ? s * (ut.y / nut) : T(0), fr ? s * (ut.z / nut) : T(0)};
-    const V3<T> P = {jn * n.x + jt.x, jn * n.y + jt.y, jn * n.z + jt.z};
-    const V3<T> dw = np_matvec(invI, np_cross(r, P));
-    const bool go = live && !(un >= T(0));
-    v = {go ? v.x + P.x / m : v.x, go ? v.y + P.y / m : v.y, go ? v.z + P.z / m : v.z};
-    w = {go ? w.x + dw.x : w.x, go ? w.y + dw.y : w.y, go ? w.z + dw.z : w.z};
-}
-
 // ---- MuJoCo semantics (contact generation, quaternion integration) --------
 template <typename T> __device__ __forceinline__ T mj_dot(V3<T> a, V3<T> b) {
     return a.x * b.x + a.y * b.y + a.z * b.z;

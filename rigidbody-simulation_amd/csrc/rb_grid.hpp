@@ -483,10 +483,12 @@ __device__ __forceinline__ int32_t search_buckets(const StepParams<T> &p, int32_
 #define RB_WIDE_LDSPOS 1
 #endif
 constexpr int WIDE_HPOS = 8;
-// the rare path (buckets of 7+ bodies) software-pipelined over its batches
-// (0: each batch's ids, then its snapshots)
+// the rare path (buckets of 7+ bodies) software-pipelined over its batches,
+// its cursor in registers (2; 1: the cursor walked through LDS, C4 pile-up
+// 60.5 -> 55.1 us for 2, C3 unchanged, profiles/r04/rare_cursor_*; 0: each
+// batch's ids, then its snapshots)
 #ifndef RB_WIDE_PIPE
-#define RB_WIDE_PIPE 1
+#define RB_WIDE_PIPE 2
 #endif
 // diagnostic (0): the wide search skips buckets' ids past the head (wrong
 // for a bucket of 7+ bodies); measures the rare path's code footprint

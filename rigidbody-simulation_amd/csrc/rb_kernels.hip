@@ -341,11 +341,6 @@ template <typename T> struct Lead {
 #ifndef RB_SOLVE_PIPE
 #define RB_SOLVE_PIPE 1
 #endif
-// the wide sphere kernels: each partner batch's contact geometry computed
-// first, then its solves branch-free (impulse_apply_sel), in one basic block
-#ifndef RB_SOLVE_FLAT
-#define RB_SOLVE_FLAT 0
-#endif
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 template <typename T>
@@ -458,38 +453,6 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             if (s0 + PB < np_) fetch(s0 + PB, jn, sn_next);
         } else {
             fetch(s0, jj, pe);
-        }
-        if constexpr (!BOXES && RB_SOLVE_FLAT && PM == 2) {
-            // the batch's geometry (step-start data only), then its
-            // sequential solves; padding entries solve nothing
-            Contact<T> cn[PB];
-            V3<T> nn[PB];
-#pragma unroll
-            for (int u = 0; u < PB; ++u)
-                if (s0 + u >= np_) {                         // (fetch leaves them unset)
-                    jj[u] = i;
-                    pe[u] = Snap<T>{x.x + T(1), x.y, x.z, sz.x};
-                }
-#pragma unroll
-            for (int u = 0; u < PB; ++u) {
-                const V3<T> cj = {pe[u].x, pe[u].y, pe[u].z};
-                const bool lo = i < jj[u];                   // this body is geom1
-                sphere_sphere(lo ? x : cj, lo ? sz.x : pe[u].r, lo ? cj : x, lo ? pe[u].r : sz.x, cn[u]);
-                nn[u] = (lo && p.oriented) ? V3<T>{-cn[u].frame.x, -cn[u].frame.y, -cn[u].frame.z} : cn[u].frame;
-            }
-            if (p.rec_count) {
-#pragma unroll
-                for (int u = 0; u < PB; ++u)
-                    if (s0 + u < np_) record(p, l, nrec, jj[u], 16, cn[u].dist);
-            }
-            const M3<T> &iI = invI.get();
-#pragma unroll
-            for (int u = 0; u < PB; ++u) {
-                const bool live = s0 + u < np_ && cn[u].dist < T(0) && !(absval(cn[u].dist) < p.thr);
-                const V3<T> r = {cn[u].pos.x - x.x, cn[u].pos.y - x.y, cn[u].pos.z - x.z};
-                impulse_apply_sel(live, k, m, iI, r, nn[u], p.e, p.mu, v, w);
-            }
-            continue;
         }
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
