@@ -341,6 +341,11 @@ template <typename T> struct Lead {
 #ifndef RB_SOLVE_PIPE
 #define RB_SOLVE_PIPE 1
 #endif
+// batches of partner snapshots in flight ahead of the solve (the helper-wave
+// wide form only: its register budget has room for a second batch)
+#ifndef RB_SOLVE_DEPTH
+#define RB_SOLVE_DEPTH 1
+#endif
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 template <typename T>
@@ -365,7 +370,7 @@ __device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T
 // the discovery index d = pdidx[u * stride] < WIDE_HPOS (LDS, PM = 2: wide
 // form) or gathered from the step-start snapshot (PM = 0, and PM = 2 past
 // WIDE_HPOS).  A template flag, so LDS accesses stay ds_read (no flat loads).
-template <typename T, int PM, bool BOXES = false>
+template <typename T, int PM, bool BOXES = false, int SDEPTH = 1>
 __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, int32_t i, V3<T> x, int32_t kind,
                                             V3<T> sz, T bi, const BodyIn<T> &in, bool forced, LazyInvI<T> &invI,
                                             int32_t np_, const int32_t *pid, int64_t stride, const Snap<T> *ppos,
@@ -439,15 +444,26 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     // sphere kernels (RB_SOLVE_PIPE): the next batch's snapshots load under
     // this batch's solves — a body with many partners (C4's pile-ups: up to
     // 28) otherwise waits one round trip per PB partners re-read from memory
-    [[maybe_unused]] int32_t jn[PB];
-    [[maybe_unused]] Snap<T> sn_next[PB];
+    [[maybe_unused]] int32_t jn[PB], jn2[PB];
+    [[maybe_unused]] Snap<T> sn_next[PB], sn_next2[PB];
     constexpr bool pipe = !BOXES && RB_SOLVE_PIPE && PM != 1;   // (the cooperative form: LDS only)
-    if constexpr (pipe)
+    constexpr bool deep = pipe && SDEPTH > 1;
+    if constexpr (pipe) {
         if (np_ > 0) fetch(0, jn, sn_next);
+        if constexpr (deep)
+            if (np_ > PB) fetch(PB, jn2, sn_next2);
+    }
     for (int s0 = 0; s0 < np_; s0 += PB) {
         int32_t jj[PB];
         Snap<T> pe[PB];
-        if constexpr (pipe) {
+        if constexpr (deep) {
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {
+                jj[u] = jn[u]; pe[u] = sn_next[u];
+                jn[u] = jn2[u]; sn_next[u] = sn_next2[u];
+            }
+            if (s0 + 2 * PB < np_) fetch(s0 + 2 * PB, jn2, sn_next2);
+        } else if constexpr (pipe) {
 #pragma unroll
             for (int u = 0; u < PB; ++u) { jj[u] = jn[u]; pe[u] = sn_next[u]; }
             if (s0 + PB < np_) fetch(s0 + PB, jn, sn_next);
@@ -683,10 +699,11 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
         help_nrec = help_planes ? (int32_t)pr : 0;
     }
     constexpr int PM = G > 1 ? 1 : (WIDE && RB_WIDE_LDSPOS) ? 2 : 0;
-    body_update<T, PM, BOXES>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB,
-                              PM == 2 ? s_hpos + slot : s_pos + slot, tid, cell, gen + 1u,
-                              BOXES ? s_poly + slot : nullptr, NB, PM == 2 ? s_didx + slot : nullptr, help_nrec,
-                              help_planes);
+    constexpr int SD = (WIDE && HELP) ? RB_SOLVE_DEPTH : 1;
+    body_update<T, PM, BOXES, SD>(p, l, i, x, kind, sz, bi, in, forced, invI, np_, s_id + slot, NB,
+                                  PM == 2 ? s_hpos + slot : s_pos + slot, tid, cell, gen + 1u,
+                                  BOXES ? s_poly + slot : nullptr, NB, PM == 2 ? s_didx + slot : nullptr, help_nrec,
+                                  help_planes);
 }
 
 // Halo exchange: fold the wave's new cells, given as per-lane boxes
