@@ -41,6 +41,11 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][16];
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
         __builtin_amdgcn_sched_barrier(0);                                                        \
         if (tid == 0 && blockIdx.x < (1u << 16)) rb_stamp_buf[blockIdx.x][k] = t_;                \
+        if (k == 0 || k == 6) { /* the constant-rate clock too, comparable across XCDs */            \
+            unsigned long long r_;                                                                \
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory");        \
+            if (tid == 0 && blockIdx.x < (1u << 16)) rb_stamp_buf[blockIdx.x][k == 0 ? 12 : 13] = r_; \
+        }                                                                                         \
     } while (0)
 #else
 #define STAMP(k) do {} while (0)

@@ -70,6 +70,7 @@ for step in "$@"; do
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
         stampsc4) run stamps_c4 300 python -u scripts/stamps_c4.py --warm 700 ;;
+        stampsc3) run stamps_c3 300 python -u scripts/stamps_c4.py --config c3 --warm 30 ;;
         framecost) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 ;;
         framecostq) run frame_cost 300 python -u scripts/frame_cost.py --config c3 --frames 20 --skip-drift ;;
         framecost8) run frame_cost_t8 300 env RBHIP_HOST_THREADS=8 python -u scripts/frame_cost.py --config c3 --frames 20 --skip-drift ;;

@@ -49,6 +49,14 @@ def main():
           f"block total median {int(np.median(tot))} p99 {int(np.percentile(tot, 99))} max {int(tot.max())}; "
           f"blocks over 2x median {int((tot > 2 * np.median(tot)).sum())} of {nb}; "
           f"sphere partners per body max {int(nss.max())} mean {nss.mean():.2f}")
+    # s_memrealtime (100 MHz, one clock for the chip) at the first and last
+    # stamp: when blocks start and end relative to the first start, in us
+    st, en = (b[:, 12] - b[:, 12].min()) / 100.0, (b[:, 13] - b[:, 12].min()) / 100.0
+    q = lambda a: " ".join(f"{np.percentile(a, x):.2f}" for x in (0, 10, 50, 90, 99, 100))
+    print(f"  block start us (p0 p10 p50 p90 p99 max): {q(st)}")
+    print(f"  block end   us (p0 p10 p50 p90 p99 max): {q(en)}")
+    print(f"  block length us (median): {np.median(en - st):.2f}; cycles per us (memtime / realtime): "
+          f"{np.median(tot / np.maximum(en - st, 1e-3)):.0f}")
     for label, rows in (("median", None), ("slowest", order[:5])):
         for lo, hi, nm in phases:
             d = b[:, hi] - b[:, lo]
