@@ -25,33 +25,15 @@ for step in "$@"; do
         xbtimec2) run xb_time_c2 300 python -u scripts/xb_time.py --config c2 --ks 0,2,4,6,8,12,16 ;;
         xbtimec4) run xb_time_c4 300 python -u scripts/xb_time.py --config c4 --start 260 --ks 0,4,8 ;;
         shims) run shims 300 python -u -m pytest tests/test_gpu_shims.py tests/test_gpu_threads.py -x -q --timeout 300 --timeout-method thread ;;
-        c4ab) run c4_pipe_ab 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_pipe0.so" SCENE=incline \
-              SIZES=256x256 WARM=500 ENVS=RBHIP_XB=0 ROUNDS=2 python -u scripts/ablate.py ;;
         xsmp) run xs_mp 600 python -u -m pytest tests/test_gpu_shard_mp.py -x -v -k "sharded_blocks or two_process_shards_match_single_world and p2p" --timeout 300 --timeout-method thread ;;
         xbl1) run xb_tests_l1 600 env RBHIP_LIB_PATH=build/xb_l1.so python -u -m pytest tests/test_gpu_xblock.py -x -q --timeout 300 --timeout-method thread &&
               run xb_time_l1 300 env RBHIP_LIB_PATH=build/xb_l1.so python -u scripts/xb_time.py --ks 0,8,16 &&
               run xb_time_l1_8k 300 env RBHIP_LIB_PATH=build/xb_l1.so python -u scripts/xb_time.py --config slab8k --ks 0,8,16 &&
               run xb_stamps_l1 300 python -u scripts/xb_stamps.py --lib build/xbstamps_l1.so --config c3 --k 8 ;;
-        linkab) run link_ab_c3 300 env "LIBS=build/ab_oldlink.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=flat \
-              SIZES=256x256,128x256,256x32 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
-              run link_ab_c4 300 env "LIBS=build/ab_oldlink.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
-              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
         spab) run slotpos_ab_c3 300 env LIBS=rigidbody-simulation_amd/rbhip/librbhip.so "ENVS=RBHIP_SLOTPOS=1;RBHIP_SLOTPOS=0" SCENE=flat SIZES=256x256,128x256 WARM=20 \
               ROUNDS=3 python -u scripts/ablate.py &&
               run slotpos_ab_c4 300 env LIBS=rigidbody-simulation_amd/rbhip/librbhip.so "ENVS=RBHIP_SLOTPOS=1;RBHIP_SLOTPOS=0" SCENE=incline SIZES=256x256 WARM=500 \
               ROUNDS=2 python -u scripts/ablate.py ;;
-        sortab) run sort_ab_c3 300 env "LIBS=build/ab_prevsort.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=flat \
-              SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
-              run sort_ab_c4 300 env "LIBS=build/ab_prevsort.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
-              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
-        rankab) run rank_ab_c3 300 env "LIBS=build/ab_rank1.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=flat \
-              SIZES=256x256,128x256,256x32 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
-              run rank_ab_c4 300 env "LIBS=build/ab_rank1.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
-              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
-        qbab) run qb_ab_c3 300 env "LIBS=build/ab_qb16.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=flat \
-              SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
-              run qb_ab_c4 300 env "LIBS=build/ab_qb16.so;rigidbody-simulation_amd/rbhip/librbhip.so" SCENE=incline \
-              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
         rareab) run rare2_tests 600 env RBHIP_LIB_PATH=build/ab_rare2.so python -u -m pytest tests/test_gpu_parity.py -x -q \
               -k "crowded or c4_2000 or past_the_head or contact_rich or c3_bench_windows" --timeout 300 --timeout-method thread &&
               run flat_tests 600 env RBHIP_LIB_PATH=build/ab_flat.so python -u -m pytest tests/test_gpu_parity.py -x -q \
