@@ -59,8 +59,8 @@ for step in "$@"; do
         pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ;;
         benchK) run bench_k400 300 python -u bench.py --steps 400 --warmup 5 ;;
-        profdrv) run prof_driver 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_driver -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
-        profk) run prof_k400 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_prof_k400 -o run -- python bench.py --steps 400 --warmup 5 --no-cpu-baseline ;;
+        profdrv) run prof_driver 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04_prof_driver_csv -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+        profk) run prof_k400 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04_prof_k400_csv -o run -- python bench.py --steps 400 --warmup 5 --no-cpu-baseline ;;
         rehxs) run rehearse2_xs 600 env RBHIP_BENCH_BACKEND=gloo RBHIP_SHARD_TRANSPORT=p2p RBHIP_XB_WPG=16 RBHIP_BENCH_BLOCKS=1 \
                    python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                    --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline ;;
