@@ -48,6 +48,13 @@ for step in "$@"; do
               SIZES=256x256 WARM=500 ROUNDS=3 python -u scripts/ablate.py &&
               run depth_ab_c3 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_depth2.so" SCENE=flat \
               SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py ;;
+        blkab) run blk128_tests 600 env RBHIP_LIB_PATH=build/ab_blk128.so python -u -m pytest tests/test_gpu_parity.py -x -q \
+              -k "crowded or c4_2000 or past_the_head or contact_rich or c3_bench_windows or xfrc or ragged or large_scene or shard_invariance" \
+              --timeout 300 --timeout-method thread &&
+              run blk_ab_c3 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_blk128.so" SCENE=flat \
+              SIZES=256x256,128x256 WARM=20 ROUNDS=3 python -u scripts/ablate.py &&
+              run blk_ab_c4 300 env "LIBS=rigidbody-simulation_amd/rbhip/librbhip.so;build/ab_blk128.so" SCENE=incline \
+              SIZES=256x256 WARM=500 ROUNDS=2 python -u scripts/ablate.py ;;
         atomicprobe) run atomic_probe 120 ./scripts/atomic_probe ;;
         xbstamps) run xb_stamps 300 python -u scripts/xb_stamps.py --config c3 --k 8 ;;
         xbstamps8k) run xb_stamps_8k 300 python -u scripts/xb_stamps.py --config slab8k --k 8 ;;
