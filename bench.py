@@ -24,11 +24,7 @@ Scaling (body-id range shards, positions exchanged every step):
 The ranks exchange positions inside the library, peer-to-peer over xGMI,
 in one of two modes: halo pushes (each step, each rank pushes to each
 peer only its bodies within a cell of the peer's bounds) or full slice
-reads (each step); with RBHIP_BENCH_BLOCKS=1 also sharded K-step blocks
-(every K steps each rank pushes the full state of its bodies within the
-blocks' ghost band of each peer, then steps own bodies plus ghosts K times
-in XCD-resident blocks: bit-exact, slower per step on MI355X).
-Each is warmed up, validated and timed over 20 steps on the node itself;
+reads (each step).  Each is warmed up, validated and timed over 20 steps on the node itself;
 the fastest valid one runs the timed region
 (`config.exchange_probe_ms_per_step` lists them).  RCCL is the fallback
 when none validates.
@@ -48,10 +44,8 @@ roofline: algorithmic HBM bytes of the step kernel (248 B per
 sphere body-step in fp64) x owned bodies / its average launch duration.
 One rank: HIP events recorded on the world's stream (torch's current
 stream) around the timed region, which is exactly K graph-replayed
-step-kernel launches, / K (with K-step blocks: the region's time / K, the
-blocks' launches).  Several ranks: an event pair around each step-kernel
-launch over a second run of K steps (sharded blocks: the region's time / K,
-pushes included).  `traffic` /
+step-kernel launches, / K.  Several ranks: an event pair around each
+step-kernel launch over a second run of K steps.  `traffic` /
 `traffic_lower`: the PMC bounds per launch from the committed
 profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 command, profiles/collect_pmc.py), named in `traffic_source`;
@@ -264,17 +258,7 @@ class SingleWorldCheck:
         if self.rank == 0:
             import rbhip
             if self.ref is None:
-                # the reference steps with the per-step kernels (RBHIP_XB=0),
-                # independent of the K-step blocks a mode under test may use
-                saved = os.environ.get("RBHIP_XB")
-                os.environ["RBHIP_XB"] = "0"
-                try:
-                    self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype, **self.kw)
-                finally:
-                    if saved is None:
-                        del os.environ["RBHIP_XB"]
-                    else:
-                        os.environ["RBHIP_XB"] = saved
+                self.ref = rbhip.World(self.scene, device=self.device, dtype=self.dtype, **self.kw)
             self.ref.step(steps_total - self.done)
             self.done = steps_total
             q1, v1 = self.ref.get_state()
@@ -291,24 +275,20 @@ class SingleWorldCheck:
         return bool(int(t.item()))
 
 
-def step_kernel_name(stats: dict, blocked: bool = False) -> str:
+def step_kernel_name(stats: dict) -> str:
     """The kernel that stepped the timed region, as the library reports it
-    (rb_world_stats): the XCD-resident block kernel, or the per-step form."""
+    (rb_world_stats "form")."""
     from rbhip import _lib
-    if blocked:
-        return "rb::xblock_kernel"
     return _lib.FORM_NAMES.get(stats.get("form"), "?")
 
 
-def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str, blocked: bool = False):
+def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str):
     """(upper, lower, source) HBM bytes per step-kernel launch from the
     committed PMC summary (profiles/pmc_traffic.json, profiles/collect_pmc.py);
     keyed by config and dtype for one GPU, with a _p<N> suffix for strong
     shards.  (None, None, None) when that shape was never collected."""
     rel = os.path.join("profiles", "pmc_traffic.json")
     key = f"{cfg}_{dtype}" if P == 1 or scaling == "weak" else f"{cfg}_{dtype}_p{P}"
-    if blocked:
-        key += "_xb"                 # the block kernel's figures, per step
     try:
         with open(os.path.join(ROOT, rel)) as f:
             e = json.load(f).get(key)
@@ -376,27 +356,17 @@ def main():
     else:
         cands, probes = [], {}
         # last resort: torch.distributed's all-gather per step (host-driven)
-        # (the sharded K-step blocks, validated but measured slower per step
-        # than the per-step kernels on one GPU, DESIGN §4.2 / §6: probed only
-        # with RBHIP_BENCH_BLOCKS=1)
-        modes = [("p2p", True, False), ("p2p", False, False)]
-        if os.environ.get("RBHIP_BENCH_BLOCKS") == "1":
-            modes.append(("p2p", False, True))
-        for tr, halo, blocks in modes + [("rccl", "auto", False), ("nccl", False, False)]:
+        for tr, halo in [("p2p", True), ("p2p", False), ("rccl", "auto"), ("nccl", False)]:
             if tr in ("rccl", "nccl") and cands:
                 break
             try:
-                c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo, blocks=blocks,
+                c = ShardedWorld(scene, dtype=args.dtype, device=device, transport=tr, halo=halo,
                                  **WORLD_KW.get(args.config, {}))
-            except Exception as ex:      # (the blocks need a sphere world's mailbox)
+            except Exception as ex:
                 if rank == 0:
-                    print(f"bench: {tr} {'blocks ' if blocks else ''}unavailable: {ex}", file=sys.stderr, flush=True)
+                    print(f"bench: {tr} unavailable: {ex}", file=sys.stderr, flush=True)
                 continue
-            if blocks and not c.blocks:
-                c.world.close()
-                continue
-            name = c.transport + (" blocks" if c.blocks else " halo" if c.halo else
-                                  " full reads" if c.transport == "p2p" else "")
+            name = c.transport + (" halo" if c.halo else " full reads" if c.transport == "p2p" else "")
             c.step(args.warmup)
             if not check(c, args.warmup):
                 if rank == 0:
@@ -438,9 +408,6 @@ def main():
     elapsed = time.perf_counter() - t0
     region_ms = ev0.elapsed_time(ev1)
     st1 = w.stats()
-    # XCD-resident K-step blocks (rb_xblock.hip): every timed step committed
-    # by blocks, none rolled back
-    blocked = st1.get("xb_steps", 0) - st0.get("xb_steps", 0) == args.steps
     timed = [done + args.steps + 1, done + 2 * args.steps]
     if P > 1:
         t = torch.tensor([elapsed], device=dev_red, dtype=torch.float64)
@@ -453,14 +420,7 @@ def main():
     # region is exactly K back-to-back step-kernel launches (graph replay),
     # so HIP events around it / K.  Several ranks: a step also runs the
     # exchange, so time each step-kernel launch with its own event pair.
-    if blocked:
-        # one launch steps K reference steps: the timed region is exactly the
-        # run's block launches, so its HIP-event time / K steps is the time
-        # per step (rocprofv3's per-launch average / K agrees)
-        avg_ms, launches = region_ms / args.steps, st1["xb_launches"] - st0["xb_launches"]
-        timing = ("HIP events around the timed region / K steps (XCD-resident blocks of xb_k steps per launch: "
-                  "achieved = algorithmic bytes of the K steps / region time)")
-    elif P == 1:
+    if P == 1:
         avg_ms, launches, timing = region_ms / args.steps, args.steps, "HIP events around the timed region / K"
     else:
         w.kernel_timing(True)
@@ -471,7 +431,7 @@ def main():
     bytes_per_launch = w.bytes_per_body_step * w.n_owned
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic, traffic_lower, traffic_src, traffic_same_build = traffic_from_profiles(args.config, args.dtype, P,
-                                                                                    args.scaling, blocked)
+                                                                                    args.scaling)
 
     value = scene.n * args.steps / elapsed
     line = {
@@ -490,9 +450,7 @@ def main():
         "timed_steps": timed,
         "config": {"workload": desc, "bodies_total": scene.n, "bodies_per_gpu": w.n_owned,
                    "parallelism": f"body-range shards x{P}" + (
-                       (f", {sw.transport} ghost pushes every {w.stats()['xb_k']} steps, XCD-resident blocks, "
-                        "graph-replayed" if sw.blocks else
-                        f", {sw.transport}{' halo' if sw.halo else ''} position exchange, graph-replayed")
+                       f", {sw.transport}{' halo' if sw.halo else ''} position exchange, graph-replayed"
                        if P > 1 else ""),
                    "timed_steps": timed,
                    "dt": scene.dt, "restitution": scene.restitution, "friction": scene.friction,
@@ -504,17 +462,11 @@ def main():
                      "traffic_source": traffic_src,
                      # the counters were collected on this very library build
                      "traffic_same_build": traffic_same_build,
-                     "kernel": step_kernel_name(st1, blocked),
+                     "kernel": step_kernel_name(st1),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},
     }
-    if blocked:
-        line["roofline"]["algorithmic_bytes_per_launch"] = None
-        line["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
-    if blocked:
-        line["xblock"] = {"steps_per_launch": st1["xb_k"],
-                          **{k: st1[k] - st0[k] for k in ("xb_runs", "xb_launches", "xb_steps", "xb_fallbacks")}}
     if rank == 0 and P == 1 and not args.no_cpu_baseline:
         w.close()
         base, ref = cpu_baseline(args.config, args.cpu_steps)

@@ -215,25 +215,6 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len);
  * rb_p2p_connect and before stepping.  enable = 0 returns to full reads. */
 int rb_p2p_halo(rb_world *w, int32_t enable);
 
-/* Sharded K-step blocks (every rank alike, after rb_p2p_connect):
- * mode 1 steps rb_shard_run calls of >= 2 steps (sphere worlds, the MuJoCo
- * law, no applied forces, <= 16 partners) K steps per launch — each rank
- * pushes to each peer the full state of its bodies within the blocks' ghost
- * band of that peer's bodies, then steps its own bodies plus the ghosts K
- * times in XCD-resident blocks (rb_xblock.hip).  Bit-exact with the
- * per-step exchange; a run whose speed bound fails anywhere rolls back on
- * every rank and replays per step.  0: per-step exchange (default).
- * RB_EUNSUPPORTED: box worlds, or a mailbox made with RBHIP_XS=0.
- * Replaces, for sharded runs, the per-step loop of multi_sphere_bounce.py:42-92
- * like rb_shard_run. */
-int rb_shard_blocks(rb_world *w, int32_t mode);
-
-/* Diagnostic: the last K-step block launch's phase stamps (s_memrealtime,
- * 100 MHz), 8 per workgroup — start, speed bound, counts, map, copy, step 0,
- * last step, end — for n_wg workgroups (8 x wpg of them: workgroup b is
- * group b % 8); *wpg receives the workgroups per group. */
-int rb_diag_xb_stamps(rb_world *w, uint64_t *out, int32_t n_wg, int32_t *wpg);
-
 /* ---- the two-ball law -------------------------------------------------- */
 /* Switch a world to RB_LAW_BALLS (or back to RB_LAW_MUJOCO), replacing
  * step_with_custom_collisions (ball_collision.py:73-125): gravity v += g dt;
@@ -299,47 +280,30 @@ int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in,
  * since the last reset (HIP events on the world's stream; enable first). */
 int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
 
-/* Retired in round 4: the LDS tile blocks of round 3.  Kept
- * for ABI compatibility: mode -1 (auto) and 0 (off) are accepted and do
- * nothing; mode 1 returns RB_EUNSUPPORTED.  Long runs of sphere worlds step
- * in XCD-resident K-step blocks instead (RBHIP_XB; RB_STAT_XB_*). */
-int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned);
-
 /* Counters for tests and measurement; fills out[0 .. min(n, RB_STATS_COUNT))
- * and returns how many (the RB_STAT_TILE* slots 1-7 and 9-14 read 0: the
- * tile path was retired in round 4): */
-#define RB_STAT_GRAPHS        0   /* captured step graphs alive               */
-#define RB_STAT_TILE_RUNS     1   /* rb_step calls that ran tile blocks        */
-#define RB_STAT_TILE_BLOCKS   2   /* tile block launches that did work         */
-#define RB_STAT_TILE_REDO_T   3   /* blocks redone: an owned body was tainted  */
-#define RB_STAT_TILE_REDO_B   4   /* blocks redone: a body left its bound      */
-#define RB_STAT_TILE_RESTART  5   /* blocks rebuilt at horizon 1               */
-#define RB_STAT_TILE_FALLBACK 6   /* runs finished on the per-step kernels     */
-#define RB_STAT_TILE_STEPS    7   /* steps committed by tile blocks            */
-#define RB_STAT_FORM          8   /* per-step kernel form (0 one-lane, 1 cooperative, 2 wide, 3 cooperative + helper, 4 wide + helper) */
-#define RB_STAT_TILES         9   /* tiles of the grid                         */
-#define RB_STAT_TILE_THREADS 10   /* threads (stepped bodies) per tile         */
-#define RB_STAT_TILE_KMAX    11
-#define RB_STAT_TILE_CAP     12   /* bodies per tile bin                       */
-#define RB_STAT_TILE_SIZE_UM 13   /* tile edge in micrometres                  */
-#define RB_STAT_TILE_ON      14   /* a long rb_step would use tile blocks now  */
-#define RB_STAT_BOX_OPT      15   /* box worlds: chunks replayed without the box kernel */
-#define RB_STAT_BOX_ROLLBACK 16   /* of which rolled back and replayed with it (a body was deferred) */
-#define RB_STAT_REFITS       17   /* broadphase layout refits of a drifting scene (chunk rolled back, replayed) */
-#define RB_STAT_TABLE_GROWS  18   /* of which with the bucket table doubled */
-#define RB_STAT_BUCKETS      19   /* buckets per table now */
-#define RB_STAT_MAX_PARTNERS 20   /* max_partners now (16 -> 32 after an overflow in a guarded chunk) */
-#define RB_STAT_XB_RUNS      21   /* rb_step calls that ran XCD-resident K-step blocks */
-#define RB_STAT_XB_LAUNCHES  22   /* block launches enqueued                 */
-#define RB_STAT_XB_STEPS     23   /* steps committed by blocks (checked)     */
-#define RB_STAT_XB_FALLBACKS 24   /* block runs rolled back and replayed per step */
-#define RB_STAT_XB_K         25   /* steps per block launch                  */
-#define RB_STAT_XB_ON        26   /* a long rb_step would use the blocks now */
-#define RB_STAT_IO_SKIPPED   27   /* rb_set_state calls that were no-ops (the bytes rb_get_state handed out) */
-#define RB_STAT_IO_UPLOADS   28   /* rb_set_state calls that uploaded          */
-#define RB_STAT_XB_WHY       29   /* why bits of the block runs rolled back (OR; 1 speed, 2 capacity,
-                                     4 placement, 8 time-out, 16 other error) */
-#define RB_STATS_COUNT       30
+ * and returns how many: */
+#define RB_STAT_GRAPHS          0   /* captured step graphs alive               */
+#define RB_STAT_FORM            1   /* step kernel form of the next run: 0 one-lane, 1 cooperative, 2 wide,
+                                       3 cooperative + helper, 4 wide + helper (hashed cells),
+                                       5 cell-ordered tiles (rb_tiles.hip) */
+#define RB_STAT_BOX_OPT         2   /* box worlds: chunks replayed without the box kernel */
+#define RB_STAT_BOX_ROLLBACK    3   /* of which rolled back and replayed with it (a body was deferred) */
+#define RB_STAT_REFITS          4   /* broadphase layout refits of a drifting scene (chunk rolled back, replayed) */
+#define RB_STAT_TABLE_GROWS     5   /* of which with the bucket table doubled */
+#define RB_STAT_BUCKETS         6   /* buckets per table now */
+#define RB_STAT_MAX_PARTNERS    7   /* max_partners now (16 -> 32 after an overflow in a guarded chunk) */
+#define RB_STAT_IO_SKIPPED      8   /* rb_set_state calls that were no-ops (the bytes rb_get_state handed out) */
+#define RB_STAT_IO_UPLOADS      9   /* rb_set_state calls that uploaded          */
+#define RB_STAT_TILE_RUNS      10   /* runs stepped in the cell-ordered tile form */
+#define RB_STAT_TILE_STEPS     11   /* steps of those runs committed (checked)  */
+#define RB_STAT_TILE_ROLLBACKS 12   /* tile runs rolled back and replayed by the hashed-cell forms */
+#define RB_STAT_TILE_BUILDS    13   /* tile bins built from the id-ordered state */
+#define RB_STAT_TILE_WHY       14   /* why bits of the rolled-back tile runs (OR; 1 bin capacity, 2 window
+                                       capacity, 4 far list, 8 partners, 16 position) */
+#define RB_STAT_TILE_SLOTS     15   /* tile slots of the periodic tile grid (workgroups per step) */
+#define RB_STAT_TILE_COLS      16   /* columns per tile edge                    */
+#define RB_STAT_TILE_ON        17   /* the next run of >= 2 steps would use the tile form */
+#define RB_STATS_COUNT         18
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

@@ -242,47 +242,6 @@ struct rb_world {
     struct GraphEntry { hipGraphExec_t ex; uint64_t used; };
     std::map<std::tuple<int64_t, int, double, double, double, double, int>, GraphEntry> graphs;
     uint64_t graph_tick = 0;
-    // XCD-resident K-step blocks (rb_xblock.hip): sphere worlds
-    // of the wide form on one rank
-    // 0 off (the default: at C3 the blocks measured 39 us per step against
-    // 16 us for the per-step kernels, profiles/r04/xb_time_c3.log), 1 on,
-    // -1 auto (RBHIP_XB=-1: worlds of >= RBHIP_XB_MIN_BODIES)
-    int xb_mode = 0;
-    int xb_k = 8;                  // steps per launch (RBHIP_XB_K)
-    int xb_wpg = 0;                // workgroups per group (CUs / 8; 0: the device cannot run the blocks)
-    int64_t xb_min_bodies = 32768; // auto mode: fewer bodies step with the per-step kernels
-    int32_t xb_cap = 0;            // local bodies per group
-    int xb_axis = 0;               // slab axis
-    double xb_cut[XB_GROUPS + 1] = {};
-    bool xb_cut_valid = false;
-    double xb_valpha = 1.5, xb_vbeta = 0.5;   // speed bound of a launch (m/s): valpha max|v| + vbeta + K |g| dt
-    void *xb_sp = nullptr;         // [XB_GROUPS][4] StepParams<T> (device)
-    std::vector<char> xb_sp_host;  // the last upload (skipped when unchanged)
-    int32_t *xb_map = nullptr, *xb_lkind = nullptr;
-    void *xb_lsnap = nullptr, *xb_lstate = nullptr, *xb_lconst = nullptr;
-    uint32_t *xb_lines = nullptr;  // [XB_GROUPS][2][H][32] the groups' bucket tables
-    uint32_t *xb_spill = nullptr;  // [XB_GROUPS][2][2 + 2 SPILL_CAP]
-    int64_t xb_H = 0;              // buckets of those tables (their own linear layout, xb_group)
-    int32_t xb_group = 0;          // Grid::super of the block tables (8 x 8 x 4 cell groups, 4 heads per line)
-    XbCtl *xb_ctl = nullptr;
-    bool xb_pending = false;       // a run awaits its check (xb_finish)
-    int64_t xb_c0 = 0, xb_n = 0;
-    double xb_prm[4] = {};
-    int64_t xb_stats[4] = {};      // runs, launches, steps committed, runs rolled back and replayed per step
-    int32_t xb_backoff = 0;        // eligible runs to skip after a roll-back (doubles)
-    int32_t xb_skip = 0;
-    int32_t xb_why = 0;            // XB_WHY_* of the runs rolled back (OR), 16: another error bit
-    bool xb_sharded = false;       // the pending run is a sharded one (XS)
-    // sharded K-step blocks (XS: rb_p2p.hip xs_push_kernel + the blocks'
-    // sharded form): peer-to-peer worlds, every rank alike
-    int xs_mode = 0;               // rb_shard_blocks: 0 off, 1 on
-    bool xs_mail = false;          // the mailbox lays out the XS regions (sphere worlds, RBHIP_XS != 0)
-    unsigned long long *xs_gidx = nullptr;   // [XB_GROUPS][Npad]
-    float *xs_part = nullptr;      // [push blocks][8]
-    unsigned long long *xs_done = nullptr;   // [2]
-    int32_t *xs_push_cnt = nullptr, *xs_in_cnt = nullptr;   // [P], [P]
-    int64_t *xs_epoch = nullptr;
-    void *xs_vw = nullptr;         // [2] T: the launch's V, W
     // the boundary's staging (rb_set_state / rb_get_state): pinned host rows
     // in the caller's layout and their device twins, moved with one DMA each
     // way and transposed by a kernel.  The staging mirrors the device state
@@ -538,7 +497,7 @@ template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
     hp.push_cnt = w->push_cnt;
     hp.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
     hp.mail = reinterpret_cast<const char *>(w->flags);
-    hp.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
+    hp.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
     hp.epoch = w->epoch;
     hp.rank = (int32_t)w->rank;
     hp.P = (int32_t)w->P;
@@ -639,12 +598,10 @@ int gen_guard(rb_world *w, int64_t nsteps) {
     return RB_OK;
 }
 
-int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false,
-                  bool allow_xb = true);
+int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false);
 
-int xb_finish(rb_world *w);
-// every run that awaits its check at the next sync point (block runs)
-int finish_pending(rb_world *w) { return xb_finish(w); }
+// every run that awaits its check at the next sync point
+int finish_pending(rb_world *) { return RB_OK; }
 
 // Guarded chunks (enqueue_steps): the chunk-start copy (state rows,
 // snapshot, box orientations, error word), the check after the chunk (error
@@ -887,404 +844,8 @@ inline void best_period_split(const std::vector<PeriodSet> &sets, const double n
         }
 }
 
-// ---- XCD-resident K-step blocks (rb_xblock.hip) ----------------
-bool xb_eligible(const rb_world *w, int64_t nsteps) {
-    if (w->xb_mode == 0 || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
-        return false;
-    if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;   // (N <= 16,384 x wpg)
-    if (nsteps < 2) return false;
-    return w->xb_mode == 1 || w->N >= w->xb_min_bodies;
-}
-
-// the slabs: equal body counts along the widest horizontal axis (x, y) of
-// the n positions qpos (stride 7); group g owns [cut[g], cut[g+1]).  Fewer
-// than XB_GROUPS bodies, or a non-finite position: group 0 owns everything
-// (the block launch then reports the position; a shard's choice must not
-// differ from its peers', so the blocks still run)
-void xb_fit_cuts(rb_world *w, const double *qpos, int64_t stride, int64_t n) {
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-    bool finite = true;
-    for (int64_t b = 0; b < n; ++b)
-        for (int d = 0; d < 3; ++d) {
-            const double u = qpos[stride * b + d];
-            if (!(u == u) || fabs(u) > 1e12) { finite = false; continue; }
-            lo[d] = std::min(lo[d], u);
-            hi[d] = std::max(hi[d], u);
-        }
-    w->xb_cut[0] = -INFINITY;
-    for (int g = 1; g <= XB_GROUPS; ++g) w->xb_cut[g] = INFINITY;
-    w->xb_axis = (hi[1] - lo[1]) > (hi[0] - lo[0]) ? 1 : 0;
-    if (finite && n >= XB_GROUPS) {
-        std::vector<double> u((size_t)n);
-        for (int64_t b = 0; b < n; ++b) u[(size_t)b] = qpos[stride * b + w->xb_axis];
-        for (int g = 1; g < XB_GROUPS; ++g) {
-            const size_t k = (size_t)(n * g / XB_GROUPS);
-            std::nth_element(u.begin(), u.begin() + k, u.end());
-            const double below = *std::max_element(u.begin(), u.begin() + k);
-            w->xb_cut[g] = 0.5 * (below + u[k]);
-        }
-    }
-    // the block tables' layout: groups of 8 x 8 x 4 cells laid out linearly
-    // (rb_grid.hpp bucket_linear), the period split scored like the world's
-    // (fit_period), by the collisions within each group's copy (its slab
-    // and an estimated band: a group's table holds only its copy)
-    const int gb[3] = {3, 3, 2};
-    int lg = 0;
-    while ((int64_t(1) << (lg + 1)) <= w->xb_H) ++lg;
-    lg -= gb[0] + gb[1] + gb[2];
-    double need[3] = {1.0, 1.0, 1.0};
-    const double band = 1.5 * w->xb_k * 2.0 * w->rmax;
-    std::vector<std::vector<int64_t>> occ(XB_GROUPS);
-    for (int g = 0; g < XB_GROUPS; ++g) {
-        const double rlo = g == 0 ? -INFINITY : w->xb_cut[g] - band, rhi = g == XB_GROUPS - 1 ? INFINITY : w->xb_cut[g + 1] + band;
-        double glo[3] = {1e300, 1e300, 1e300}, ghi[3] = {-1e300, -1e300, -1e300};
-        for (int64_t b = 0; b < n; ++b) {
-            const double u = qpos[stride * b + w->xb_axis];
-            if (!(u >= rlo && u < rhi)) continue;
-            int64_t c[3];
-            bool ok = true;
-            for (int d = 0; d < 3; ++d) {
-                const double v = qpos[stride * b + d] * w->inv_cs;
-                if (!(v == v && v > -1e9 && v < 1e9)) { ok = false; break; }
-                glo[d] = std::min(glo[d], v);
-                ghi[d] = std::max(ghi[d], v);
-                c[d] = (int64_t)floor(v) >> gb[d];
-            }
-            if (ok) occ[(size_t)g].push_back(period_pack(c[0], c[1], c[2]));
-        }
-        for (int d = 0; d < 3; ++d)
-            if (ghi[d] >= glo[d]) need[d] = std::max(need[d], (floor(ghi[d]) - floor(glo[d]) + 2) / double(1 << gb[d]));
-    }
-    std::vector<PeriodSet> sets;
-    for (auto &o : occ) sets.emplace_back(std::move(o));
-    int l[3] = {lg, 0, 0};
-    best_period_split(sets, need, lg, l);
-    const int32_t grp = 0x233 | (l[0] << 12) | (l[1] << 16) | (l[2] << 20) | (1 << 24) | (2 << 25);
-    if (grp != w->xb_group) w->xb_sp_host.clear();       // (the step parameters carry the grid)
-    w->xb_group = grp;
-    w->xb_cut_valid = true;
-}
-
-// the slabs fitted to the positions of the current step (the snapshot; a
-// shard: its own bodies)
-int xb_refit_cuts(rb_world *w) {
-    const int64_t n = w->n_local, lo = w->lo;
-    std::vector<double> q((size_t)7 * (n > 0 ? n : 1), 0.0);
-    const size_t ne = (size_t)4 * n;
-    HIPCHK(hipStreamSynchronize(w->stream));
-    if (w->dtype == RB_F64) {
-        std::vector<double> sn(ne);
-        HIPCHK(hipMemcpy(sn.data(), dp<double>(w->snap[w->sp()], 4 * lo), sizeof(double) * ne, hipMemcpyDeviceToHost));
-        for (int64_t b = 0; b < n; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; q[(size_t)(7 * b + 2)] = sn[(size_t)(4 * b + 2)]; }
-    } else {
-        std::vector<float> sn(ne);
-        HIPCHK(hipMemcpy(sn.data(), dp<float>(w->snap[w->sp()], 4 * lo), sizeof(float) * ne, hipMemcpyDeviceToHost));
-        for (int64_t b = 0; b < n; ++b) { q[(size_t)(7 * b)] = sn[(size_t)(4 * b)]; q[(size_t)(7 * b + 1)] = sn[(size_t)(4 * b + 1)]; q[(size_t)(7 * b + 2)] = sn[(size_t)(4 * b + 2)]; }
-    }
-    double old[XB_GROUPS + 1];
-    memcpy(old, w->xb_cut, sizeof old);
-    const int old_axis = w->xb_axis;
-    const int32_t old_group = w->xb_group;
-    xb_fit_cuts(w, q.data(), 7, n);
-    if (memcmp(old, w->xb_cut, sizeof old) != 0 || old_axis != w->xb_axis || old_group != w->xb_group)
-        drop_graphs(w);                                  // the cuts are captured kernel arguments
-    return RB_OK;
-}
-
-// the groups' buffers (lazily, at the first eligible run; the tables again
-// when the world's table size changes)
-int xb_alloc(rb_world *w) {
-    if (w->xb_ctl) return RB_OK;
-    HIPCHK(hipStreamSynchronize(w->stream));
-    drop_graphs(w);
-    if (!w->xb_ctl) {
-        // one group per XCD, one workgroup per CU
-        int cus = 0;
-        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, w->device));
-        w->xb_wpg = (cus % XB_GROUPS == 0 && cus / XB_GROUPS >= 1 && cus / XB_GROUPS <= XB_MAX_WPG) ? cus / XB_GROUPS : 0;
-        // RBHIP_XB_WPG=n (tests): n workgroups per group, so that the launches
-        // of ranks sharing one GPU fit on it together (2 x 16 per XCD)
-        if (const char *ev = getenv("RBHIP_XB_WPG")) {
-            const int v = atoi(ev);
-            if (w->xb_wpg && v >= 1 && v <= w->xb_wpg) w->xb_wpg = v;
-        }
-        if (!w->xb_wpg) return RB_OK;
-        // room for the slab and a band of up to half its width on each side
-        // (a wider copy fails the block: the chunk replays step by step)
-        // (a shard: its own bodies' slab plus own and pushed ghosts)
-        const int64_t own = w->P > 1 ? w->n_local : w->N;
-        int64_t cap = std::min<int64_t>(w->N, 2 * ((own + XB_GROUPS - 1) / XB_GROUPS) + 8192);
-        cap = (cap + 63) / 64 * 64;
-        w->xb_cap = (int32_t)cap;
-        const size_t esz = (size_t)w->esz;
-        HIPCHK(hipMalloc((void **)&w->xb_map, sizeof(int32_t) * XB_GROUPS * cap));
-        HIPCHK(hipMalloc((void **)&w->xb_lkind, sizeof(int32_t) * XB_GROUPS * cap));
-        HIPCHK(hipMalloc(&w->xb_lsnap, esz * 4 * 2 * XB_GROUPS * cap));
-        HIPCHK(hipMalloc(&w->xb_lstate, esz * 13 * XB_GROUPS * cap));
-        HIPCHK(hipMalloc(&w->xb_lconst, esz * 8 * XB_GROUPS * cap));
-        HIPCHK(hipMalloc((void **)&w->xb_spill, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
-        HIPCHK(hipMemset(w->xb_spill, 0, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
-        HIPCHK(hipMalloc((void **)&w->xb_ctl, sizeof(XbCtl)));
-        HIPCHK(hipMemset(w->xb_ctl, 0, sizeof(XbCtl)));
-        const size_t spb = (w->dtype == RB_F64 ? sizeof(StepParams<double>) : sizeof(StepParams<float>)) * XB_GROUPS * 4;
-        HIPCHK(hipMalloc(&w->xb_sp, spb));
-        // 32 buckets per local body (as the wide form's tables), 2^14 .. 2^22
-        w->xb_H = std::min<int64_t>(std::max<int64_t>(next_pow2(32 * cap), int64_t(1) << 14), int64_t(1) << 22);
-    }
-    // the tables: generation-tagged like the world's (nothing is cleared), so
-    // a fresh allocation is zeroed and every group starts at generation 2
-    if (w->xb_lines) { HIPCHK(hipFree(w->xb_lines)); w->xb_lines = nullptr; }
-    const size_t words = (size_t)XB_GROUPS * 2 * LINE_WORDS * (size_t)w->xb_H;
-    HIPCHK(hipMalloc((void **)&w->xb_lines, sizeof(uint32_t) * words));
-    HIPCHK(hipMemset(w->xb_lines, 0, sizeof(uint32_t) * words));
-    HIPCHK(hipMemset(w->xb_spill, 0, sizeof(uint32_t) * XB_GROUPS * 2 * (2 + 2 * SPILL_CAP)));
-    std::vector<uint32_t> gen((size_t)XB_GROUPS * 32, 2u);
-    HIPCHK(hipMemcpy(w->xb_ctl->gen, gen.data(), sizeof(uint32_t) * gen.size(), hipMemcpyHostToDevice));
-    w->xb_sp_host.clear();
-    return RB_OK;
-}
-
-// the groups' step parameters: [g][v], v = parity | (last step ? 2 : 0);
-// uploaded when they change (step parameters, the grid)
-template <typename T> int xb_upload_params(rb_world *w, double dt, double e, double mu, double thr) {
-    std::vector<StepParams<T>> sp((size_t)XB_GROUPS * 4);
-    const int64_t cap = w->xb_cap;
-    for (int g = 0; g < XB_GROUPS; ++g)
-        for (int v = 0; v < 4; ++v) {
-            const int par = v & 1;
-            StepParams<T> p = make_step<T>(w, 0, dt, e, mu, thr, true);
-            Snap<T> *ls = dp<Snap<T>>(w->xb_lsnap, 0) + (int64_t)g * 2 * cap;
-            p.snap_cur = ls + par * cap;
-            p.snap_next = ls + (1 - par) * cap;
-            p.st = BodyState<T>{dp<T>(w->xb_lstate, 0) + (int64_t)g * 13 * cap, cap};
-            p.cs = BodyConsts<T>{dp<T>(w->xb_lconst, 0) + (int64_t)g * 8 * cap, cap, w->xb_lkind + (int64_t)g * cap};
-            p.n_local = (int32_t)cap;
-            p.lo = 0;
-            p.n_global = cap;
-            p.S = (int32_t)cap;
-            p.xfrc = nullptr;
-            p.grid.hmask = (uint32_t)(w->xb_H - 1);
-            p.grid.H = (int32_t)w->xb_H;
-            p.grid.super = w->xb_group;
-            auto tab = [&](int q) {
-                return Table<T>{w->xb_lines + ((size_t)(2 * g + q) * LINE_WORDS * (size_t)w->xb_H), nullptr, nullptr,
-                                w->xb_spill + (size_t)(2 * g + q) * (2 + 2 * SPILL_CAP)};
-            };
-            p.cur = tab(par);
-            p.next = v >= 2 ? Table<T>{nullptr, nullptr, nullptr, nullptr} : tab(1 - par);
-            p.epoch = nullptr;
-            p.bounds = nullptr;
-            p.plist = nullptr;
-            p.plist_cnt = nullptr;
-            p.rec_count = nullptr; p.rec_partner = nullptr; p.rec_kind = nullptr; p.rec_dist = nullptr;
-            p.maxrec = 0;
-            p.quat_cur = nullptr; p.quat_next = nullptr;
-            p.defer_q = nullptr; p.defer_cnt = nullptr; p.defer_reset = nullptr;
-            p.vel_cur = nullptr; p.vel_next = nullptr;
-            sp[(size_t)(4 * g + v)] = p;
-        }
-    const size_t bytes = sizeof(StepParams<T>) * sp.size();
-    if (w->xb_sp_host.size() == bytes && memcmp(w->xb_sp_host.data(), sp.data(), bytes) == 0) return RB_OK;
-    HIPCHK(hipStreamSynchronize(w->stream));
-    HIPCHK(hipMemcpy(w->xb_sp, sp.data(), bytes, hipMemcpyHostToDevice));
-    w->xb_sp_host.assign(reinterpret_cast<const char *>(sp.data()), reinterpret_cast<const char *>(sp.data()) + bytes);
-    return RB_OK;
-}
-
-template <typename T> XbParams<T> make_xb(rb_world *w, int64_t c, int K, double dt) {
-    XbParams<T> p{};
-    p.sp = static_cast<const StepParams<T> *>(w->xb_sp);
-    p.snap_in = dp<Snap<T>>(w->snap[c % 2], 0);
-    p.snap_out = dp<Snap<T>>(w->snap[(c + K) % 2], 0);
-    p.st_base = dp<T>(w->state, 0);
-    p.S = w->S;
-    p.cs = BodyConsts<T>{dp<T>(w->consts, 0), w->Npad, w->kind};
-    p.n = (int32_t)w->N;
-    p.axis = w->xb_axis;
-    for (int g = 0; g <= XB_GROUPS; ++g) p.cut[g] = (T)w->xb_cut[g];
-    p.K = K;
-    p.wpg = w->xb_wpg;
-    p.cap = w->xb_cap;
-    p.reach = (T)(2.0 * w->rmax);
-    p.gdt = (T)(sqrt(w->g[0] * w->g[0] + w->g[1] * w->g[1] + w->g[2] * w->g[2]) * dt);
-    p.valpha = (T)w->xb_valpha;
-    p.vbeta = (T)w->xb_vbeta;
-    p.map = w->xb_map;
-    p.lsnap = dp<Snap<T>>(w->xb_lsnap, 0);
-    p.lstate = dp<T>(w->xb_lstate, 0);
-    p.lconst = dp<T>(w->xb_lconst, 0);
-    p.lkind = w->xb_lkind;
-    p.ctl = w->xb_ctl;
-    p.err = w->err;
-    p.timeout_ticks = 50000000;        // 0.5 s at 100 MHz
-    if (w->P > 1) {                    // sharded (XS): own rows at id - lo, ghosts from the mailbox
-        p.xs = 1;
-        p.lo = (int32_t)w->lo;
-        p.n_local = (int32_t)w->n_local;
-        p.P = (int32_t)w->P;
-        p.mail = reinterpret_cast<const char *>(w->flags);
-        p.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
-        p.in_cnt = w->xs_in_cnt;
-        p.vw = static_cast<const T *>(w->xs_vw);
-        p.xs_epoch = w->xs_epoch;
-        p.gidx = w->xs_gidx;
-        p.Npad = w->Npad;
-    }
-    return p;
-}
-
-template <typename T> XsPushParams<T> make_xs_push(rb_world *w, int64_t c, int K, double dt) {
-    XsPushParams<T> p{};
-    p.snap = dp<Snap<T>>(w->snap[c % 2], 0);
-    p.st = BodyState<T>{dp<T>(w->state, 0), w->S};
-    p.lo = (int32_t)w->lo;
-    p.n_local = (int32_t)w->n_local;
-    p.rank = (int32_t)w->rank;
-    p.P = (int32_t)w->P;
-    p.S = w->S;
-    p.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
-    p.mail = reinterpret_cast<char *>(w->flags);
-    p.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
-    p.part = w->xs_part;
-    p.done = w->xs_done;
-    p.push_cnt = w->xs_push_cnt;
-    p.xs_epoch = w->xs_epoch;
-    p.vw = static_cast<T *>(w->xs_vw);
-    p.in_cnt = w->xs_in_cnt;
-    p.K = K;
-    p.reach = (T)(2.0 * w->rmax);
-    p.gdt = (T)(sqrt(w->g[0] * w->g[0] + w->g[1] * w->g[1] + w->g[2] * w->g[2]) * dt);
-    p.dt = (T)dt;
-    p.valpha = (T)w->xb_valpha;
-    p.vbeta = (T)w->xb_vbeta;
-    p.err = w->err;
-    p.timeout_ticks = 500000000;       // 5 s at 100 MHz (as the per-step exchange)
-    return p;
-}
-
-// the launches of n block steps from step c0 on stream s: xb_k steps each
-int xb_enqueue(rb_world *w, hipStream_t s, int64_t c0, int64_t n, double dt) {
-    for (int64_t done = 0; done < n;) {
-        const int K = (int)std::min<int64_t>(w->xb_k, n - done);
-        const hipError_t r = w->dtype == RB_F64 ? launch_xblock<double>(make_xb<double>(w, c0 + done, K, dt), w->maxp, s)
-                                                : launch_xblock<float>(make_xb<float>(w, c0 + done, K, dt), w->maxp, s);
-        HIPCHK(r);
-        done += K;
-    }
-    return RB_OK;
-}
-
-// Sharded (XS): per block of K steps, the push kernel (headers, ghosts,
-// counts: rb_p2p.hip) and the block launch; after the run's last block a
-// final push (headers and counts only: every rank learns whether any rank
-// failed, and that every peer's last block committed) and the gather of
-// every peer's snapshot slice, so the per-step path finds the whole scene.
-int xs_enqueue(rb_world *w, hipStream_t s, int64_t c0, int64_t n, double dt) {
-    const bool f64 = w->dtype == RB_F64;
-    for (int64_t done = 0; done < n;) {
-        const int K = (int)std::min<int64_t>(w->xb_k, n - done);
-        HIPCHK(f64 ? launch_xs_push<double>(make_xs_push<double>(w, c0 + done, K, dt), s)
-                   : launch_xs_push<float>(make_xs_push<float>(w, c0 + done, K, dt), s));
-        HIPCHK(f64 ? launch_xblock<double>(make_xb<double>(w, c0 + done, K, dt), w->maxp, s)
-                   : launch_xblock<float>(make_xb<float>(w, c0 + done, K, dt), w->maxp, s));
-        done += K;
-    }
-    const int64_t ce = c0 + n;
-    HIPCHK(f64 ? launch_xs_push<double>(make_xs_push<double>(w, ce, 0, dt), s)
-               : launch_xs_push<float>(make_xs_push<float>(w, ce, 0, dt), s));
-    const int sp = (int)(ce % 2);
-    if (f64)
-        HIPCHK(launch_xs_gather<double>(dp<Snap<double>>(w->snap[sp], 0),
-                                        reinterpret_cast<const Snap<double> *const *>(w->peer_snap_dev + sp * w->P),
-                                        (int32_t)w->rank, (int32_t)w->P, w->S, w->N, s));
-    else
-        HIPCHK(launch_xs_gather<float>(dp<Snap<float>>(w->snap[sp], 0),
-                                       reinterpret_cast<const Snap<float> *const *>(w->peer_snap_dev + sp * w->P),
-                                       (int32_t)w->rank, (int32_t)w->P, w->S, w->N, s));
-    return RB_OK;
-}
-
-bool xs_eligible(const rb_world *w, int64_t nsteps) {
-    if (w->xs_mode != 1 || w->P < 2 || !w->p2p || !w->xs_mail || !w->all_spheres || w->law != RB_LAW_MUJOCO ||
-        w->xfrc || w->timing)
-        return false;
-    if (w->xb_wpg < 0 || w->maxp > 16 || w->N > (int64_t(1) << 18)) return false;
-    return nsteps >= 2;
-}
-
-// A run of n steps in blocks: the chunk-start state is saved (the blocks
-// commit in place), the launches replay from a graph, and the run is checked
-// at the next sync point (xb_finish; at once for a synchronous rb_step).
-int xb_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
-    const bool sh = w->P > 1;                // sharded (XS): every rank runs the same launches
-    if (int rc = xb_alloc(w)) return rc;
-    if (!w->xb_cut_valid)
-        if (int rc = xb_refit_cuts(w)) return rc;
-    if (!w->xb_wpg) {
-        w->xb_mode = 0;                      // the device cannot run the blocks
-        w->xs_mode = 0;
-        return enqueue_steps(w, n, dt, e, mu, thr, sh, false);
-    }
-    int rc = w->dtype == RB_F64 ? xb_upload_params<double>(w, dt, e, mu, thr) : xb_upload_params<float>(w, dt, e, mu, thr);
-    if (rc) return rc;
-    if ((rc = chunk_save(w))) return rc;
-    rc = sh ? graph_replay(w, n, 9, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) { return xs_enqueue(w, s, c0, n, dt); })
-            : graph_replay(w, n, 8, dt, e, mu, thr, [&](hipStream_t s, int64_t c0) { return xb_enqueue(w, s, c0, n, dt); });
-    if (rc) return rc;
-    w->xb_pending = true;
-    w->xb_sharded = sh;
-    w->xb_c0 = w->c;
-    w->xb_n = n;
-    w->xb_prm[0] = dt; w->xb_prm[1] = e; w->xb_prm[2] = mu; w->xb_prm[3] = thr;
-    w->c += n;
-    w->primed = false;                       // the world's own table is stale
-    w->xb_stats[0] += 1;
-    w->xb_stats[1] += (n + w->xb_k - 1) / w->xb_k;
-    if (w->sync_call) return xb_finish(w);
-    return RB_OK;
-}
-
-// The check of a block run: any error raised during it (ERR_XB: an
-// assumption of the blocks failed; or any other bit) rolls the chunk back
-// to its start and replays it with the per-step kernels, which report real
-// errors themselves.  After a roll-back the next eligible runs step per step
-// (a doubling back-off); a capacity failure refits the slabs to the current
-// positions, a placement or time-out failure turns the blocks off.
-int xb_finish(rb_world *w) {
-    if (!w->xb_pending) return RB_OK;
-    w->xb_pending = false;
-    int32_t err = 0;
-    bool deferred = false;
-    if (int rc = chunk_check(w, err, deferred)) return rc;
-    if (!err) {
-        w->xb_stats[2] += w->xb_n;
-        if (w->xb_backoff > 0) w->xb_backoff /= 2;
-        return RB_OK;
-    }
-    w->xb_stats[3] += 1;
-    XbCtl ctl;
-    HIPCHK(hipMemcpy(&ctl, w->xb_ctl, sizeof ctl, hipMemcpyDeviceToHost));
-    // barrier counters and the poison word back to a clean start (the
-    // generations stay: they only grow)
-    HIPCHK(hipMemset(w->xb_ctl, 0, offsetof(XbCtl, cnt)));
-    HIPCHK(hipMemset(&w->xb_ctl->poison, 0, 2 * sizeof(int32_t)));
-    // (a shard: every rank rolled back alike — the push kernels spread an
-    // error to every rank — and must keep deciding alike, so only the
-    // back-off, which every rank advances the same way, applies)
-    w->xb_why |= ctl.why | ((err & ~ERR_XB) ? 16 : 0);
-    if (!w->xb_sharded && (ctl.why & (XB_WHY_PLACEMENT | XB_WHY_TIMEOUT))) w->xb_mode = 0;
-    w->xb_backoff = w->xb_backoff ? std::min(2 * w->xb_backoff, 64) : 1;
-    w->xb_skip = w->xb_backoff;
-    w->c = w->xb_c0;
-    if (int rc = chunk_restore(w)) return rc;
-    if (ctl.why & XB_WHY_CAP) w->xb_cut_valid = false;   // the slabs drifted: refit at the next run
-    const double *q = w->xb_prm;
-    return enqueue_steps(w, w->xb_n, q[0], q[1], q[2], q[3], w->xb_sharded, false);
-}
-
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
-int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded,
-                  bool allow_xb) {
+int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
     if (!sharded && w->P != 1) return fail(RB_EINVAL, "rb_step on a sharded world: use rb_shard_run or rb_shard_step + exchange");
     if (sharded && !w->comm && !w->p2p) return fail(RB_EINVAL, "rb_shard_run before rb_shard_comm_init or rb_p2p_connect");
@@ -1295,18 +856,6 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     w->state_version += 1;
-    if (allow_xb && (sharded ? xs_eligible(w, w->record ? nsteps - 1 : nsteps)
-                             : xb_eligible(w, w->record ? nsteps - 1 : nsteps))) {
-        if (w->xb_skip > 0) {
-            --w->xb_skip;                        // (back-off after a roll-back: this run steps per step)
-        } else {
-            int rc = xb_run(w, w->record ? nsteps - 1 : nsteps, dt, e, mu, thr);
-            if (rc || !w->record) return rc;
-            // the recorded (last) step runs on the per-step kernels
-            if ((rc = finish_pending(w))) return rc;
-            nsteps = 1;
-        }
-    }
     if (int rc = gen_guard(w, nsteps)) return rc;
     if (!w->primed || (w->law == RB_LAW_BALLS && (dt != w->prm_dt || e != w->prm_e || mu != w->prm_mu))) {
         int rc = prime(w, dt, e, mu);
@@ -1584,11 +1133,7 @@ void free_world(rb_world *w) {
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
-    void *tbufs[] = {w->opt_save, w->xb_sp, w->xb_map, w->xb_lkind, w->xb_lsnap,
-                     w->xb_lstate, w->xb_lconst, w->xb_lines, w->xb_spill, w->xb_ctl,
-                     w->xs_gidx, w->xs_part, w->xs_done, w->xs_push_cnt, w->xs_in_cnt, w->xs_epoch, w->xs_vw};
-    for (void *b : tbufs)
-        if (b) (void)hipFree(b);
+    if (w->opt_save) (void)hipFree(w->opt_save);
     if (w->defer_host) (void)hipHostFree(w->defer_host);
     if (w->io_q_h) (void)hipHostFree(w->io_q_h);
     if (w->io_v_h) (void)hipHostFree(w->io_v_h);
@@ -1672,13 +1217,6 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_HELP")) w->wide_help = atoi(ev) != 0;
-    // XCD-resident K-step blocks (rb_xblock.hip): RBHIP_XB = 0 off (default),
-    // 1 on, -1 auto (sphere worlds of >= RBHIP_XB_MIN_BODIES)
-    if (const char *ev = getenv("RBHIP_XB")) w->xb_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
-    if (const char *ev = getenv("RBHIP_XB_K")) w->xb_k = std::max(1, std::min(64, atoi(ev)));
-    if (const char *ev = getenv("RBHIP_XB_MIN_BODIES")) w->xb_min_bodies = atoll(ev);
-    if (const char *ev = getenv("RBHIP_XB_VALPHA")) w->xb_valpha = atof(ev);
-    if (const char *ev = getenv("RBHIP_XB_VBETA")) w->xb_vbeta = atof(ev);
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
@@ -1822,7 +1360,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
 
 void rb_world_destroy(rb_world *w) {
     ApiScope api_scope_;
-    if (w && w->xb_pending) {
+    if (w) {
         (void)hipSetDevice(w->device);
         (void)hipStreamSynchronize(w->stream);
     }
@@ -1930,7 +1468,6 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     HIPCHK(hipStreamSynchronize(w->stream));     // (a DMA out of the staging may be in flight)
     par_copy2(w->io_q_h, qpos, nq, w->io_v_h, qvel, nv);
     fit_period(w, qpos);
-    w->xb_cut_valid = false;                             // block slabs: refitted at the next block run
     HIPCHK(hipMemcpyAsync(w->io_q_d, w->io_q_h, sizeof(double) * nq, hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(w->io_v_d, w->io_v_h, sizeof(double) * nv, hipMemcpyHostToDevice, w->stream));
     const hipError_t e = w->dtype == RB_F64 ? launch_state_in<double>(make_io<double>(w), w->stream)
@@ -2132,11 +1669,8 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
     HIPCHK(hipSetDevice(w->device));
     if (!w->flags) {
         // the mailbox, uncached: peers write it over xGMI while this rank's
-        // kernels poll and read it.  Sphere worlds lay out the sharded
-        // blocks' regions too (RBHIP_XS=0: not; every rank must agree)
-        const char *xe = getenv("RBHIP_XS");
-        w->xs_mail = !w->boxes && !(xe && atoi(xe) == 0) && w->P <= 64;
-        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes, w->xs_mail);
+        // kernels poll and read it
+        const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
         HIPCHK(hipExtMallocWithFlags((void **)&w->flags, (size_t)lay.bytes, hipDeviceMallocUncached));
         HIPCHK(hipMemset(w->flags, 0, (size_t)lay.bytes));
     }
@@ -2201,52 +1735,6 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     HIPCHK(hipDeviceSynchronize());
     w->p2p = true;
     drop_graphs(w);
-    return RB_OK;
-}
-
-// diagnostic: the last block launch's phase stamps, [workgroups][8]
-int rb_diag_xb_stamps(rb_world *w, uint64_t *out, int32_t n_wg, int32_t *wpg) {
-    ApiScope api_scope_;
-    if (!w || !out) return fail(RB_EINVAL, "null argument");
-    if (!w->xb_ctl) return fail(RB_EINVAL, "no block launch yet");
-    HIPCHK(hipSetDevice(w->device));
-    HIPCHK(hipStreamSynchronize(w->stream));
-    const int32_t nw = std::min<int32_t>(n_wg, XB_GROUPS * XB_MAX_WPG);
-    HIPCHK(hipMemcpy(out, w->xb_ctl->stamp, sizeof(uint64_t) * XB_STAMPS * nw, hipMemcpyDeviceToHost));
-    if (wpg) *wpg = w->xb_wpg;
-    return RB_OK;
-}
-
-// Sharded K-step blocks (XS): every rank of a peer-to-peer world
-// alike.  The buffers are made at the first enable.
-int rb_shard_blocks(rb_world *w, int32_t mode) {
-    ApiScope api_scope_;
-    if (!w) return fail(RB_EINVAL, "null world");
-    if (mode != 0 && mode != 1) return fail(RB_EINVAL, "mode must be 0 or 1");
-    HIPCHK(hipSetDevice(w->device));
-    if (int rc = finish_pending(w)) return rc;
-    if (mode == 1) {
-        if (!w->p2p) return fail(RB_EINVAL, "rb_shard_blocks before rb_p2p_connect");
-        if (!w->xs_mail) return fail(RB_EUNSUPPORTED, "sharded blocks: sphere worlds whose mailbox lays them out (RBHIP_XS != 0)");
-        if (!w->xs_gidx) {
-            HIPCHK(hipStreamSynchronize(w->stream));
-            const int64_t nb = std::max<int64_t>(1, (w->n_local + XS_PUSH_BLOCK - 1) / XS_PUSH_BLOCK);
-            HIPCHK(hipMalloc((void **)&w->xs_gidx, sizeof(unsigned long long) * XB_GROUPS * w->Npad));
-            HIPCHK(hipMemset(w->xs_gidx, 0, sizeof(unsigned long long) * XB_GROUPS * w->Npad));
-            HIPCHK(hipMalloc((void **)&w->xs_part, sizeof(float) * 8 * nb));
-            HIPCHK(hipMalloc((void **)&w->xs_done, sizeof(unsigned long long) * 2));
-            HIPCHK(hipMemset(w->xs_done, 0, sizeof(unsigned long long) * 2));
-            HIPCHK(hipMalloc((void **)&w->xs_push_cnt, sizeof(int32_t) * w->P));
-            HIPCHK(hipMemset(w->xs_push_cnt, 0, sizeof(int32_t) * w->P));
-            HIPCHK(hipMalloc((void **)&w->xs_in_cnt, sizeof(int32_t) * w->P));
-            HIPCHK(hipMemset(w->xs_in_cnt, 0, sizeof(int32_t) * w->P));
-            HIPCHK(hipMalloc((void **)&w->xs_epoch, sizeof(int64_t)));
-            HIPCHK(hipMemset(w->xs_epoch, 0, sizeof(int64_t)));
-            HIPCHK(hipMalloc(&w->xs_vw, 2 * sizeof(double)));
-        }
-    }
-    if (w->xs_mode != mode) drop_graphs(w);
-    w->xs_mode = mode;
     return RB_OK;
 }
 
@@ -2450,29 +1938,15 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
 
 extern "C" {
 
-// The LDS tile blocks of round 3 were retired in round 4: the
-// XCD-resident blocks (rb_xblock.hip) replace them.  The entry stays for ABI
-// compatibility: mode -1 / 0 are accepted (nothing to configure), 1 fails.
-int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned) {
-    ApiScope api_scope_;
-    if (!w) return fail(RB_EINVAL, "null world");
-    if (mode < -1 || mode > 1 || kmax < 0 || kmax > 64 || !(band >= 0) || owned < 0)
-        return fail(RB_EINVAL, "bad tile configuration");
-    if (mode == 1) return fail(RB_EUNSUPPORTED, "the LDS tile blocks were retired; the XCD-resident blocks replace them");
-    return RB_OK;
-}
-
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     ApiScope api_scope_;
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
     const int form = step_form(w);
-    const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), 0, 0, 0, 0, 0, 0, 0, form, 0, 0, 0, 0, 0, 0,
-                                       w->box_stats[0], w->box_stats[1], w->refits, w->table_grows, w->H,
-                                       (int64_t)w->maxp, w->xb_stats[0], w->xb_stats[1], w->xb_stats[2], w->xb_stats[3],
-                                       (int64_t)w->xb_k, xb_eligible(w, 1 << 20) ? 1 : 0, w->io_stats[0], w->io_stats[1],
-                                       (int64_t)w->xb_why};
+    const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), form, w->box_stats[0], w->box_stats[1], w->refits,
+                                       w->table_grows, w->H, (int64_t)w->maxp, w->io_stats[0], w->io_stats[1],
+                                       0, 0, 0, 0, 0, 0, 0, 0};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

@@ -60,52 +60,9 @@ __device__ __forceinline__ int64_t chk(int64_t idx, int64_t n, int line) {
 }
 #define CHK(idx, n) chk((idx), (n), __LINE__)
 
-// Loads of data another workgroup of the SAME launch may have written (the
-// step-start snapshot, bucket heads and slots, the spill list): plain loads
-// in the per-step kernels, whose writers are all in the previous launch.  In
-// the XCD-resident block kernel (rb_xblock.hip, RB_XB) the steps follow each
-// other inside one launch, separated by a barrier among the workgroups of one
-// XCD: there they must bypass the CU's vector L1, which is never refreshed by
-// another CU's stores, and are served by the XCD's L2, which every writer
-// shares (MI355X_MICROARCH.md, inter-workgroup visibility; scripts/xb_probe.hip).
-#ifndef RB_XB
-#define RB_XB 0
-#endif
-// XCD-resident loads: 1 = sc1 (agent-scope relaxed atomic loads, 8 bytes
-// each), 2 = nt 16-byte loads, 0 = plain loads (L1-cached: the block kernel
-// then invalidates each CU's L1 after every barrier, rb_xblock.hip)
-#ifndef RB_XB_LD
-#define RB_XB_LD 1
-#endif
-template <typename V> __device__ __forceinline__ V xld(const V *p) {
-#if RB_XB && RB_XB_LD != 0
-    static_assert(sizeof(V) % 4 == 0, "xld: whole words");
-    V v;
-    if constexpr (RB_XB_LD == 2 && sizeof(V) % 16 == 0) {
-        using u4 = __attribute__((ext_vector_type(4))) unsigned;
-        u4 t[sizeof(V) / 16];
-#pragma unroll
-        for (size_t k = 0; k < sizeof(V) / 16; ++k) t[k] = __builtin_nontemporal_load(reinterpret_cast<const u4 *>(p) + k);
-        __builtin_memcpy(&v, t, sizeof(V));
-    } else if constexpr (sizeof(V) % 8 == 0) {
-        unsigned long long t[sizeof(V) / 8];
-#pragma unroll
-        for (size_t k = 0; k < sizeof(V) / 8; ++k)
-            t[k] = __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p) + k, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_memcpy(&v, t, sizeof(V));
-    } else {
-        unsigned t[sizeof(V) / 4];
-#pragma unroll
-        for (size_t k = 0; k < sizeof(V) / 4; ++k)
-            t[k] = __hip_atomic_load(reinterpret_cast<const unsigned *>(p) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_memcpy(&v, t, sizeof(V));
-    }
-    return v;
-#else
-    return *p;
-#endif
-}
+// Loads of step-start data (the snapshot, bucket heads and slots, the spill
+// list): every writer of it ran in the previous launch, so plain loads.
+template <typename V> __device__ __forceinline__ V xld(const V *p) { return *p; }
 
 constexpr uint32_t N_XCD = 8;
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {

@@ -202,21 +202,6 @@ template <typename T> struct P2PParams {
     T *qdst;
 };
 
-// Sharded K-step blocks (XS; rb_p2p.hip xs_push_kernel, rb_xblock.hip):
-// every K steps each rank pushes to each peer the full state of its bodies
-// within the blocks' band W of that peer's own bodies, into the peer's
-// mailbox (two parities); the peer's block launch copies them as ghosts.
-//   int64  xhdr[P][XS_HDR_WORDS]  peer q's header of epoch e, (e << 32) | bits:
-//                                 x min, x max, y min, y max (float, rounded
-//                                 outward), max |v| (float, rounded up), error
-//   int64  xcnt[P]                bodies peer q pushed, (e << 32) | count
-//   uint32 xids[2][P][xg]         pushed global ids (parity e % 2)
-//   T      xpay[2][P][XS_PAY][xg] their snapshot (x y z r) and 13 state rows
-constexpr int XS_HDR_WORDS = 6;
-constexpr int XS_PAY = 17;
-constexpr int64_t XS_GHOST_MAX = 32768;   // bodies one peer pushes to this rank per block at most
-constexpr int XS_PUSH_BLOCK = 256;
-
 // Halo exchange (rb_p2p.hip), for large shards: instead of reading every
 // peer's whole slice, each rank PUSHES to each peer only its bodies whose
 // cell lies within one cell of that peer's own bodies' cell bounds — a
@@ -240,9 +225,7 @@ constexpr int BOUND_STRIDE = 32;       // int32 per copy (128 B): min x y z, max
 // stale one without a separate flag (and a release fence before it).
 struct MailLayout {
     int64_t o_flags, o_box, o_cnt, o_ids, o_snap, o_quat, bytes;   // o_quat: -1 without boxes
-    // sharded K-step blocks (XS_*, below; o_xhdr == -1: not laid out)
-    int64_t o_xhdr, o_xcnt, o_xids, o_xpay, xg;
-    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz, bool boxes, bool xs = false) {
+    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz, bool boxes) {
         MailLayout m;
         m.o_flags = 0;
         m.o_box = 8 * P;
@@ -251,16 +234,6 @@ struct MailLayout {
         m.o_snap = (m.o_ids + 4 * P * S + 255) / 256 * 256;
         m.o_quat = boxes ? m.o_snap + 4 * esz * P * S : -1;
         m.bytes = m.o_snap + (boxes ? 8 : 4) * esz * P * S;
-        m.o_xhdr = m.o_xcnt = m.o_xids = m.o_xpay = -1;
-        m.xg = 0;
-        if (xs) {
-            m.xg = S < XS_GHOST_MAX ? S : XS_GHOST_MAX;
-            m.o_xhdr = (m.bytes + 255) / 256 * 256;
-            m.o_xcnt = m.o_xhdr + 8 * XS_HDR_WORDS * P;
-            m.o_xids = (m.o_xcnt + 8 * P + 255) / 256 * 256;
-            m.o_xpay = (m.o_xids + 4 * 2 * P * m.xg + 255) / 256 * 256;
-            m.bytes = m.o_xpay + esz * 2 * P * XS_PAY * m.xg;
-        }
         return m;
     }
 };
@@ -282,113 +255,6 @@ template <typename T> struct HaloParams {
     // own boxes' rows fresh, pushed boxes' rows land here), else nullptr
     T *quat;
 };
-
-// ---- XCD-resident K-step blocks (rb_xblock.hip) -----------------
-// One launch steps the scene K times.  Its workgroups form XB_GROUPS groups
-// (blocks b, b + 8, b + 16, ... : the workgroups of one XCD, checked against
-// the XCC_ID register), one per slab of the scene along its widest horizontal
-// axis.  Each group copies its slab's bodies plus a ghost band wide enough
-// that no body outside the copy can influence an owned body within K steps
-// into buffers of its own, rebuilds its own broadphase table every step, and
-// steps the copy K times — separated by barriers among the group's
-// workgroups only, so the copy, its snapshots and its tables stay in that
-// XCD's L2 — before writing its owned bodies back.
-constexpr int XB_GROUPS = 8;
-constexpr int XB_THREADS = 512;        // one workgroup per CU: 8 waves, 2 per SIMD
-constexpr int XB_MAX_WPG = 64;         // workgroups per group at most
-constexpr int XB_STAMPS = 8;
-constexpr int32_t ERR_XB = 1 << 21;    // an assumption of a block failed (speed bound, capacity, placement,
-                                       // barrier time-out): the host rolls the chunk back and replays it with
-                                       // the per-step kernels (never user-visible)
-struct XbCtl {
-    unsigned long long bar[XB_GROUPS][16];   // group barrier arrivals, one 128-B line per group (monotone)
-    unsigned long long gathered[16];         // workgroups done gathering (monotone, every group)
-    int32_t cnt[XB_GROUPS][XB_MAX_WPG];      // loaded bodies in each workgroup's id chunk
-    uint32_t vpart[XB_GROUPS][XB_MAX_WPG];   // float bits: max |v| over each workgroup's id chunk
-    uint32_t gen[XB_GROUPS][32];             // the group's next table generation
-    uint32_t xcc[XB_GROUPS * XB_MAX_WPG];    // XCC id of each workgroup
-    int32_t poison;                          // a wait timed out: later waits are skipped
-    int32_t why;                             // XB_WHY_* bits of the failures since the last reset
-    int32_t pad0[30];
-    int32_t nload[XB_GROUPS];                // loaded bodies of each group (statistics, last launch)
-    uint32_t vmax_bits;                      // float bits: max |v| at the start of the last launch (statistics)
-    uint32_t pad1[15];
-    // s_memrealtime (100 MHz) of each workgroup of the last launch at its
-    // phase ends (rb_diag_xb_stamps): start, speed bound, counts, map,
-    // copy, step 0, last step, end (committed)
-    unsigned long long stamp[XB_GROUPS * XB_MAX_WPG][XB_STAMPS];
-};
-enum : int32_t { XB_WHY_SPEED = 1, XB_WHY_CAP = 2, XB_WHY_PLACEMENT = 4, XB_WHY_TIMEOUT = 8 };
-template <typename T> struct XbParams {
-    const StepParams<T> *sp;           // [XB_GROUPS][4]: the group's step parameters, (parity, last step)
-    const Snap<T> *snap_in;            // the scene at step c (global ids)
-    Snap<T> *snap_out;                 // the owned bodies at step c + K (== snap_in when K is even)
-    T *st_base;                        // state rows [13][S] (global ids; P == 1), in place
-    int64_t S;
-    BodyConsts<T> cs;
-    int32_t n;                         // bodies
-    int32_t axis;                      // slab axis: 0 x, 1 y
-    T cut[XB_GROUPS + 1];              // group g owns axis coordinate in [cut[g], cut[g+1]) (first / last open)
-    int32_t K;                         // steps of this launch
-    int32_t wpg;                       // workgroups per group
-    int32_t cap;                       // local bodies per group at most
-    T reach;                           // contact reach: 2 x the largest radius
-    T gdt;                             // |g| dt
-    T valpha, vbeta;                   // speed bound of a launch: valpha max|v| + vbeta + K |g| dt
-    int32_t *map;                      // [XB_GROUPS][cap] local index -> global id (ascending)
-    Snap<T> *lsnap;                    // [XB_GROUPS][2][cap] the copy's snapshots, ping-pong
-    T *lstate;                         // [XB_GROUPS][13][cap]
-    T *lconst;                         // [XB_GROUPS][8][cap]
-    int32_t *lkind;                    // [XB_GROUPS][cap]
-    XbCtl *ctl;
-    int32_t *err;
-    int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) a wait may take
-    // sharded worlds (XS; xs == 0: one rank, the fields below unused).  The
-    // own bodies [lo, lo + n_local) have their state rows at id - lo; the
-    // ghosts come from the mailbox the preceding xs_push_kernel filled
-    int32_t xs;
-    int32_t lo, n_local, P;
-    const char *mail;                  // this rank's mailbox (MailLayout lay)
-    MailLayout lay;
-    const int32_t *in_cnt;             // [P] ghosts each peer pushed for this launch (xs_push_kernel)
-    const T *vw;                       // [2] the launch's speed bound V and band W (xs_push_kernel)
-    const int64_t *xs_epoch;           // the push kernel's epoch (its parity selects the inbox)
-    unsigned long long *gidx;          // [XB_GROUPS][Npad] (epoch << 32) | inbox slot of a ghost id
-    int64_t Npad;
-};
-template <typename T> hipError_t launch_xblock(const XbParams<T> &p, int maxp, hipStream_t s);
-
-// The push before a sharded block launch (rb_p2p.hip xs_push_kernel): the
-// own bodies' bounds and max |v| to every peer, everyone's back, then the
-// own bodies within W of each peer's bounds to that peer's inbox, then the
-// counts; the kernel ends when every peer's counts of this epoch arrived
-// (so the block launch that follows never waits on a peer).
-template <typename T> struct XsPushParams {
-    const Snap<T> *snap;               // the current snapshot (own rows fresh)
-    BodyState<T> st;                   // own state rows [13][S]
-    int32_t lo, n_local, rank, P;
-    int64_t S;
-    char *const *peer_mail;            // [P] each peer's mailbox (own entry: this rank's)
-    char *mail;                        // this rank's mailbox
-    MailLayout lay;
-    float *part;                       // [blocks][8] per-block bounds / max |v| (partials)
-    unsigned long long *done;          // [2] arrivals (monotone): partials, pushes
-    int32_t *push_cnt;                 // [P]
-    int64_t *xs_epoch;                 // advanced by the kernel (read by the block launch)
-    T *vw;                             // [2] out: V, W
-    int32_t *in_cnt;                   // [P] out: ghosts each peer pushed to this rank
-    int32_t K;                         // steps of the block launch that follows (0: the final push of a run,
-                                       // headers and counts only)
-    T reach, gdt, dt, valpha, vbeta;
-    int32_t *err;
-    int64_t timeout_ticks;
-};
-template <typename T> hipError_t launch_xs_push(const XsPushParams<T> &p, hipStream_t s);
-// the end of a sharded block run: every peer's snapshot slice (final once
-// its last push counted) into the own snapshot, so the per-step kernels and
-// rb_get_state see the whole scene again
-template <typename T> hipError_t launch_xs_gather(Snap<T> *dst, const Snap<T> *const *peer_snap, int32_t rank,
-                                                  int32_t P, int64_t S, int64_t N, hipStream_t s);
 
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one

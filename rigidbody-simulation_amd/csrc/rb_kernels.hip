@@ -23,12 +23,12 @@
 #include "rb_device.hpp"
 
 // diagnostic build only: per-wave s_memtime stamps at phase boundaries.
-// One unit keeps them (the fp64 wide unit; the block unit in its own stamp
-// build): the host-side name of the buffer must be unique in the library
+// One unit keeps them (the fp64 wide unit): the host-side name of the
+// buffer must be unique in the library
 #ifndef RB_STAMPS
 #define RB_STAMPS 0
 #endif
-#if RB_STAMPS && !((defined(RB_XB) && RB_XB) || (defined(RB_WIDE_UNIT) && RB_WIDE_UNIT == 1 && defined(RB_INST) && RB_INST == 1))
+#if RB_STAMPS && !(defined(RB_WIDE_UNIT) && RB_WIDE_UNIT == 1 && defined(RB_INST) && RB_INST == 1)
 #undef RB_STAMPS
 #define RB_STAMPS 0
 #endif
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
     if (p.bounds) fold_bounds(p.bounds, cell);
 }
 
-#if RB_STAMPS && !(defined(RB_XB) && RB_XB)
+#if RB_STAMPS
 extern "C" int rb_diag_stamps(unsigned long long *out, int nblocks) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rb_stamp_buf), sizeof(unsigned long long) * 16 * nblocks);
 }

@@ -279,229 +279,6 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
     }
 }
 
-// ---- sharded K-step blocks: the push (XS; rb_internal.hpp) ----------------
-// Before each block launch of a sharded world (rb_xblock.hip, xs != 0):
-//   1. every workgroup reduces its own bodies' x / y bounds and max |v|
-//      (floats rounded outward), the last to arrive publishes the rank's
-//      header, epoch-tagged, into every mailbox (its own too);
-//   2. every workgroup waits for all P headers of this epoch; they give the
-//      launch's speed bound V = valpha max|v| + vbeta + K |g| dt over ALL
-//      ranks (so every rank bounds every body alike) and the band W;
-//   3. each own body within W of a peer's bounds (both axes) goes to that
-//      peer's inbox of this epoch's parity: its id, snapshot and 13 state
-//      rows (system-scope stores over xGMI; a wave-aggregated slot count);
-//   4. the last workgroup done pushing publishes the counts, then waits for
-//      every peer's counts of this epoch: when the kernel ends, this rank's
-//      inbox is complete, and the block launch never waits on a peer.
-// A peer writes this rank's inbox of parity e % 2 again only in its push of
-// epoch e + 2, after its block launch e + 1, which needed this rank's counts
-// of epoch e + 1, published after this rank's block launch e: one inbox per
-// parity suffices.  Headers and counts of epoch e are overwritten only after
-// this rank's push e ended likewise.  An error anywhere (this rank's error
-// word at the push, a time-out, a full inbox) goes into the header's error
-// word: every rank then raises ERR_XB, and all roll the run back together.
-__device__ __forceinline__ float f_down(double v) { return __double2float_rd(v); }
-__device__ __forceinline__ float f_up(double v) { return __double2float_ru(v); }
-__device__ __forceinline__ float f_down(float v) { return v; }
-__device__ __forceinline__ float f_up(float v) { return v; }
-
-template <typename T>
-__global__ __launch_bounds__(XS_PUSH_BLOCK) void xs_push_kernel(XsPushParams<T> p) {
-    constexpr int NW = XS_PUSH_BLOCK / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const MailLayout &L = p.lay;
-    const int64_t e = *p.xs_epoch + 1;
-    const int par = (int)(e & 1);
-    const unsigned nb = gridDim.x;
-    __shared__ float s_red[NW][6];
-    __shared__ float s_hdr[64][6];
-    __shared__ int s_last;
-
-    // 1. own partials: x min, x max, y min, y max, max |v|, error
-    const int64_t l = (int64_t)blockIdx.x * XS_PUSH_BLOCK + tid;
-    const bool act = l < p.n_local;
-    Snap<T> s{};
-    T vx = T(0), vy = T(0), vz = T(0);
-    if (act) {
-        s = p.snap[p.lo + l];
-        vx = p.st.vx()[l]; vy = p.st.vy()[l]; vz = p.st.vz()[l];
-    }
-    const T sp = sqroot(vx * vx + vy * vy + vz * vz);
-    const bool bad = act && !(s.x == s.x && s.y == s.y && sp == sp && fabs(s.x) < T(1e30) && fabs(s.y) < T(1e30) &&
-                              sp < T(1e30));
-    float b[6] = {act && !bad ? f_down(s.x) : INFINITY, act && !bad ? f_up(s.x) : -INFINITY,
-                  act && !bad ? f_down(s.y) : INFINITY, act && !bad ? f_up(s.y) : -INFINITY,
-                  act && !bad ? f_up(sp) : 0.f, bad ? 1.f : 0.f};
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        b[0] = fminf(b[0], __shfl_xor(b[0], off)); b[1] = fmaxf(b[1], __shfl_xor(b[1], off));
-        b[2] = fminf(b[2], __shfl_xor(b[2], off)); b[3] = fmaxf(b[3], __shfl_xor(b[3], off));
-        b[4] = fmaxf(b[4], __shfl_xor(b[4], off)); b[5] = fmaxf(b[5], __shfl_xor(b[5], off));
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) s_red[wave][k] = b[k];
-    __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < NW; ++w) {
-            b[0] = fminf(b[0], s_red[w][0]); b[1] = fmaxf(b[1], s_red[w][1]);
-            b[2] = fminf(b[2], s_red[w][2]); b[3] = fmaxf(b[3], s_red[w][3]);
-            b[4] = fmaxf(b[4], s_red[w][4]); b[5] = fmaxf(b[5], s_red[w][5]);
-        }
-        uint32_t *pp = reinterpret_cast<uint32_t *>(p.part) + 8 * (int64_t)blockIdx.x;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) __hip_atomic_store(pp + k, __float_as_uint(b[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        const unsigned long long old = __hip_atomic_fetch_add(p.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old % nb == nb - 1) {
-            // the last partial: the rank's header, to every mailbox
-            float h[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, 0.f, 0.f};
-            for (unsigned k = 0; k < nb; ++k) {
-                const uint32_t *q = reinterpret_cast<const uint32_t *>(p.part) + 8 * (int64_t)k;
-                float v[6];
-#pragma unroll
-                for (int j = 0; j < 6; ++j) v[j] = __uint_as_float(__hip_atomic_load(q + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                h[0] = fminf(h[0], v[0]); h[1] = fmaxf(h[1], v[1]); h[2] = fminf(h[2], v[2]);
-                h[3] = fmaxf(h[3], v[3]); h[4] = fmaxf(h[4], v[4]); h[5] = fmaxf(h[5], v[5]);
-            }
-            if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) h[5] = 1.f;
-            for (int q = 0; q < p.P; ++q) {
-                int64_t *hw = reinterpret_cast<int64_t *>(p.peer_mail[q] + L.o_xhdr) + (int64_t)XS_HDR_WORDS * p.rank;
-#pragma unroll
-                for (int j = 0; j < XS_HDR_WORDS; ++j) store_sys(hw + j, (int64_t)pack_epoch(e, (int32_t)__float_as_uint(h[j])));
-            }
-        }
-    }
-    // 2. every rank's header of this epoch
-    const int64_t *hin = reinterpret_cast<const int64_t *>(p.mail + L.o_xhdr);
-    const int nw = p.P * XS_HDR_WORDS;
-    int late = 0;
-    for (int k = tid; k < nw; k += XS_PUSH_BLOCK) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
-            const int64_t wd = load_sys(hin + k);
-            if ((int64_t)((uint64_t)wd >> 32) >= e) {
-                if ((int64_t)((uint64_t)wd >> 32) != e) late = 1;
-                s_hdr[k / XS_HDR_WORDS][k % XS_HDR_WORDS] = __uint_as_float((uint32_t)wd);
-                break;
-            }
-            if ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > p.timeout_ticks ||
-                (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_EXCHANGE)) {
-                late = 1;
-                s_hdr[k / XS_HDR_WORDS][k % XS_HDR_WORDS] = k % XS_HDR_WORDS == 5 ? 1.f : 0.f;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    if (late) atomicOr(p.err, ERR_EXCHANGE | ERR_XB);
-    __syncthreads();
-    float vm = 0.f;
-    bool any_err = false;
-    for (int q = 0; q < p.P; ++q) {
-        vm = fmaxf(vm, s_hdr[q][4]);
-        any_err |= s_hdr[q][5] != 0.f;
-    }
-    const T V = p.valpha * (T)vm + p.vbeta + (T)p.K * p.gdt;
-    const T W = (T)p.K * p.reach + T(2) * (T)(p.K > 0 ? p.K - 1 : 0) * V * p.dt + T(1e-3) * p.reach;
-    if (blockIdx.x == 0 && tid == 0) {
-        p.vw[0] = V;
-        p.vw[1] = W;
-        if (any_err) atomicOr(p.err, ERR_XB);
-    }
-
-    // 3. the own bodies each peer's blocks can reach
-    bool pushed = false;
-    if (p.K > 0 && !any_err) {
-        const int64_t G = L.xg;
-        const uint64_t lt = (1ull << lane) - 1ull;
-        for (int q = 0; q < p.P; ++q) {
-            if (q == p.rank) continue;
-            const float *h = s_hdr[q];
-            const bool in = act && !bad && h[0] <= h[1] && s.x >= (T)h[0] - W && s.x <= (T)h[1] + W &&
-                            s.y >= (T)h[2] - W && s.y <= (T)h[3] + W;
-            const uint64_t m = __ballot(in);
-            if (m == 0) continue;
-            pushed = true;
-            const int leader = __builtin_ctzll(m);
-            int32_t base = 0;
-            if (lane == leader) base = atomicAdd(p.push_cnt + q, __popcll(m));
-            base = __shfl(base, leader);
-            if (!in) continue;
-            const int64_t slot = base + __popcll(m & lt);
-            if (slot >= G) { atomicOr(p.err, ERR_XB); continue; }
-            char *mail = p.peer_mail[q];
-            uint32_t *ids = reinterpret_cast<uint32_t *>(mail + L.o_xids) + ((int64_t)par * p.P + p.rank) * G;
-            T *pay = reinterpret_cast<T *>(mail + L.o_xpay) + ((int64_t)par * p.P + p.rank) * XS_PAY * G;
-            __hip_atomic_store(ids + slot, (uint32_t)(p.lo + l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(pay + 0 * G + slot, s.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(pay + 1 * G + slot, s.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(pay + 2 * G + slot, s.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(pay + 3 * G + slot, s.r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#pragma unroll
-            for (int k = 0; k < 13; ++k)
-                __hip_atomic_store(pay + (4 + k) * G + slot, p.st.row(k)[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    // 4. the pushes are complete (acknowledged by the peers' memory); the
-    // last workgroup publishes the counts and waits for the peers'
-    if (pushed) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned long long old = __hip_atomic_fetch_add(p.done + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old % nb == nb - 1;
-        if (s_last) {
-            for (int q = 0; q < p.P; ++q) {
-                if (q == p.rank) continue;
-                const int32_t n = __hip_atomic_load(p.push_cnt + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(p.push_cnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                int64_t *cw = reinterpret_cast<int64_t *>(p.peer_mail[q] + L.o_xcnt) + p.rank;
-                store_sys(cw, (int64_t)pack_epoch(e, n < L.xg ? n : (int32_t)L.xg));
-            }
-            *p.xs_epoch = e;
-        }
-    }
-    __syncthreads();
-    if (s_last) {
-        const int64_t *cin = reinterpret_cast<const int64_t *>(p.mail + L.o_xcnt);
-        wait_peers(p.P, p.rank, e, p.timeout_ticks, p.err,
-                   [&](int q) { return (int64_t)((uint64_t)load_sys(cin + q) >> 32); });
-        if (tid < p.P) {
-            int32_t n = 0;
-            if (tid != p.rank) {
-                const int64_t wd = load_sys(cin + tid);
-                if ((int64_t)((uint64_t)wd >> 32) == e) n = (int32_t)(uint32_t)wd;
-                else atomicOr(p.err, ERR_XB);
-            }
-            p.in_cnt[tid] = n;
-        }
-    }
-}
-
-template <typename T> hipError_t launch_xs_push(const XsPushParams<T> &p, hipStream_t s) {
-    if (p.P < 1 || p.P > 64 || p.P * XS_HDR_WORDS > 64 * 6 || p.lay.o_xhdr < 0) return hipErrorInvalidValue;
-    const int64_t nb = (p.n_local + XS_PUSH_BLOCK - 1) / XS_PUSH_BLOCK;
-    hipLaunchKernelGGL((xs_push_kernel<T>), dim3((unsigned)(nb > 0 ? nb : 1)), dim3(XS_PUSH_BLOCK), 0, s, p);
-    return hipGetLastError();
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void xs_gather_kernel(Snap<T> *dst, const Snap<T> *const *peer_snap, int32_t rank,
-                                                       int64_t S, int64_t N) {
-    const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (id >= N) return;
-    const int64_t q = id / S;
-    if (q == rank) return;
-    dst[id] = load_snap_sys(peer_snap[q] + id);
-}
-
-template <typename T> hipError_t launch_xs_gather(Snap<T> *dst, const Snap<T> *const *peer_snap, int32_t rank,
-                                                  int32_t P, int64_t S, int64_t N, hipStream_t s) {
-    if (P < 1 || S <= 0 || N <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((xs_gather_kernel<T>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, dst, peer_snap, rank, S, N);
-    return hipGetLastError();
-}
-
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s) {
     if (p.P < 1 || p.P > 64 || p.S <= 0) return hipErrorInvalidValue;
     const int64_t pb = (p.n_local + 255) / 256;
@@ -523,9 +300,5 @@ template hipError_t launch_p2p_exchange<double>(const P2PParams<double> &, hipSt
 template hipError_t launch_p2p_exchange<float>(const P2PParams<float> &, hipStream_t);
 template hipError_t launch_halo_exchange<double>(const HaloParams<double> &, hipStream_t);
 template hipError_t launch_halo_exchange<float>(const HaloParams<float> &, hipStream_t);
-template hipError_t launch_xs_push<double>(const XsPushParams<double> &, hipStream_t);
-template hipError_t launch_xs_push<float>(const XsPushParams<float> &, hipStream_t);
-template hipError_t launch_xs_gather<double>(Snap<double> *, const Snap<double> *const *, int32_t, int32_t, int64_t, int64_t, hipStream_t);
-template hipError_t launch_xs_gather<float>(Snap<float> *, const Snap<float> *const *, int32_t, int32_t, int64_t, int64_t, hipStream_t);
 
 }  // namespace rb

@@ -64,8 +64,6 @@ SIGNATURES = {
     "rb_p2p_handles": (C.c_int, [_P, _P, _I64, C.POINTER(_I64)]),
     "rb_p2p_connect": (C.c_int, [_P, _P, _I64]),
     "rb_p2p_halo": (C.c_int, [_P, _I32]),
-    "rb_shard_blocks": (C.c_int, [_P, _I32]),
-    "rb_diag_xb_stamps": (C.c_int, [_P, C.c_void_p, _I32, C.POINTER(_I32)]),
     "rb_record_contacts": (C.c_int, [_P, C.c_int]),
     "rb_get_contacts": (C.c_int, [_P, _P, _P, _P, _P, _I64, C.POINTER(_I64)]),
     "rb_kat_impulse": (C.c_int, [_I32, _I32, _I64, _P, _P]),
@@ -76,18 +74,15 @@ SIGNATURES = {
     "rb_set_contact_law": (C.c_int, [_P, _I32, _D]),
     "rb_query": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     "rb_kernel_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(_I64)]),
-    "rb_tile_config": (C.c_int, [_P, _I32, _I32, _D, _I64]),
     "rb_world_stats": (C.c_int, [_P, C.POINTER(_I64), _I32]),
 }
 
 # rb_world_stats indices (include/rbhip.h RB_STAT_*)
-STAT_NAMES = ["graphs", "tile_runs", "tile_blocks", "tile_redo_taint", "tile_redo_bound", "tile_restart",
-              "tile_fallback", "tile_steps", "form", "tiles", "tile_threads", "tile_kmax", "tile_cap",
-              "tile_size_um", "tile_on", "box_opt_chunks", "box_rollbacks", "refits",
-              "table_grows", "buckets", "max_partners", "xb_runs", "xb_launches", "xb_steps",
-              "xb_fallbacks", "xb_k", "xb_on", "io_skipped", "io_uploads", "xb_why"]
+STAT_NAMES = ["graphs", "form", "box_opt_chunks", "box_rollbacks", "refits", "table_grows", "buckets",
+              "max_partners", "io_skipped", "io_uploads", "tile_runs", "tile_steps", "tile_rollbacks",
+              "tile_builds", "tile_why", "tile_slots", "tile_cols", "tile_on"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
-              3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help"}
+              3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help", 5: "rb::tile_step_kernel"}
 
 _lib = None
 

@@ -25,11 +25,7 @@ Transports:
              one captured HIP graph (SURVEY §7 hard part 4).  For large
              shards (halo="auto": >= HALO_MIN_SHARD bodies per rank) the
              halo mode instead pushes to each peer only the bodies within
-             one cell of the peer's own bodies' cell bounds.  blocks=True
-             (rb_shard_blocks) steps K steps per launch instead: every K
-             steps each rank pushes the full state of the bodies within a
-             ghost band of each peer, which then steps its own bodies plus
-             those ghosts K times in XCD-resident blocks;
+             one cell of the peer's own bodies' cell bounds;
     "rccl"   the library owns an RCCL
              communicator (id broadcast once through torch.distributed) and
              runs all three per step itself: rb_shard_run replays K steps
@@ -108,7 +104,7 @@ class ShardedWorld:
     `device`."""
 
     def __init__(self, scene: Scene, dtype: str = "f64", device: Optional[int] = None,
-                 group=None, transport: Optional[str] = None, world_factory=None, halo="auto", blocks=False,
+                 group=None, transport: Optional[str] = None, world_factory=None, halo="auto",
                  **world_kw):
         import torch
         import torch.distributed as dist
@@ -134,7 +130,6 @@ class ShardedWorld:
             self.stream = torch.cuda.current_stream(device)
             self.world.set_stream(self.stream.cuda_stream)
         self.halo = False
-        self.blocks = False
         if self.transport == "p2p":
             self._connect_p2p()
         if self.transport == "p2p":
@@ -145,12 +140,6 @@ class ShardedWorld:
             if h:
                 self.world.p2p_halo(True)
                 self.halo = True
-            # sharded K-step blocks (rb_shard_blocks): every rank alike
-            env = os.environ.get("RBHIP_XS_BLOCKS")
-            b = {"1": True, "0": False}.get(env, blocks) if env else blocks
-            if b:
-                self.world.shard_blocks(True)
-                self.blocks = True
         if self.transport == "rccl":
             # rank 0 of the group makes the communicator id, every rank joins;
             # without RCCL in this process every rank takes the torch path

@@ -192,12 +192,6 @@ class World:
         can reach); collective, after p2p_connect."""
         _lib.check(self._L.rb_p2p_halo(self._h, 1 if enable else 0), "rb_p2p_halo")
 
-    def shard_blocks(self, enable: bool = True):
-        """Sharded K-step blocks (rb_shard_blocks): shard_run calls step K
-        steps per launch with a ghost push per block; collective (every rank
-        alike), after p2p_connect."""
-        _lib.check(self._L.rb_shard_blocks(self._h, 1 if enable else 0), "rb_shard_blocks")
-
     def shard_run(self, nsteps: int = 1, dt=None, restitution=None, friction=None, threshold=None):
         """nsteps sharded steps with the in-library exchange (enqueued only)."""
         p = self._params(dt, restitution, friction, threshold)
@@ -223,15 +217,9 @@ class World:
         t = tot.value
         return cnt, par[:t], kin[:t], dis[:t]
 
-    def tile_config(self, mode: int = -1, kmax: int = 0, band: float = 0.0, owned: int = 0):
-        """Retired (rb_tile_config): mode -1 / 0 are accepted,
-        1 raises RB_EUNSUPPORTED; the XCD-resident K-step blocks replace the
-        tile blocks (stats()["xb_*"])."""
-        _lib.check(self._L.rb_tile_config(self._h, int(mode), int(kmax), float(band), int(owned)), "rb_tile_config")
-
     def stats(self) -> dict:
-        """Counters of the world (rb_world_stats): tile blocks, redos, the
-        per-step kernel form, ..."""
+        """Counters of the world (rb_world_stats, include/rbhip.h RB_STAT_*):
+        the step kernel form, tile-form runs and roll-backs, refits, ..."""
         n = len(_lib.STAT_NAMES)
         buf = (C.c_int64 * n)()
         rc = self._L.rb_world_stats(self._h, buf, n)

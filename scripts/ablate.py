@@ -18,7 +18,7 @@ for k, v in enumerate(variants if not os.environ.get("LIBS") else []):
     out = os.path.join(ROOT, "build", f"ablate{k}.so")
     if os.environ.get("PREBUILT") != "1":
         subprocess.run(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off "
-                       f"{v} -o {out} rb_kernels.hip rb_balls.hip rb_p2p.hip rb_xblock.hip rb_capi.hip", shell=True,
+                       f"{v} -o {out} rb_kernels.hip rb_balls.hip rb_p2p.hip rb_capi.hip", shell=True,
                        check=True, cwd=CSRC)
     paths[v] = out
 if os.environ.get("BUILD_ONLY") == "1":

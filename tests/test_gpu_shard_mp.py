@@ -79,59 +79,6 @@ def test_two_process_shards_match_single_world(tmp_path, P, transport, halo, pat
     assert np.array_equal(got[:, :7], q1) and np.array_equal(got[:, 7:], v1)
 
 
-# ---------------------------------------------------------------- sharded K-step blocks
-def _blocks_worker(rank, P, port, out, patch, chunks, halo):
-    for pth in (ROOT, PKG):
-        sys.path.insert(0, pth)
-    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
-    # the ranks' block launches share the one GPU: 32 / P workgroups per XCD
-    # each, so that they all fit on it at once (a launch waits at its
-    # barriers for all of its own workgroups)
-    os.environ["RBHIP_XB_WPG"] = str(32 // P - 2 * (P - 2))     # 16 at P = 2, 8 at P = 3
-    os.environ["RBHIP_XB_K"] = "6"
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=P)
-    from rbhip.shard import ShardedWorld
-    sc, kw, _ = _scene(P, patch)
-    sw = ShardedWorld(sc, device=0, transport="p2p", halo=halo, blocks=True, **kw)
-    assert sw.blocks
-    for n in chunks:
-        sw.step(n)
-    sw.sync()
-    st = sw.world.stats()
-    q, v = sw.gather_state()
-    if rank == 0:
-        np.save(out, np.concatenate([q, v], axis=1))
-        np.save(out + ".stats.npy", np.array([st["xb_steps"], st["xb_fallbacks"], st["xb_runs"], st["xb_why"]]))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("P,patch,halo,chunks", [(2, 64, False, [40, 3, 37]), (3, 48, True, [30, 30]),
-                                                 (2, "c4", False, [60, 20])])
-def test_sharded_blocks_match_single_world(tmp_path, P, patch, halo, chunks):
-    """Sharded K-step blocks (rb_shard_blocks): every 6 steps each process
-    pushes the full state of its bodies within the ghost band of each peer
-    (IPC mappings, device flags), then steps its own bodies plus ghosts in
-    XCD-resident blocks; between runs the per-step exchange takes over
-    (3-step chunk).  Bit-identical to one World, every long run committed
-    by blocks."""
-    import torch.multiprocessing as mp
-    import rbhip
-    sc, kw, _ = _scene(P, patch)
-    with rbhip.World(sc, **kw) as w:
-        w.step(sum(chunks))
-        q1, v1 = w.get_state()
-    out = str(tmp_path / "state.npy")
-    mp.start_processes(_blocks_worker, args=(P, _free_port(), out, patch, chunks, halo), nprocs=P,
-                       start_method="spawn")
-    got = np.load(out)
-    steps, fallbacks, runs, why = np.load(out + ".stats.npy")
-    assert np.array_equal(got[:, :7].view(np.uint64), q1.view(np.uint64))
-    assert np.array_equal(got[:, 7:].view(np.uint64), v1.view(np.uint64))
-    assert fallbacks == 0 and steps == sum(n for n in chunks if n >= 2), (steps, fallbacks, runs, why)
-
-
 # ---------------------------------------------------------------- in-library RCCL exchange
 # One GPU on the test box: RCCL refuses two ranks on one device, so the
 # in-library exchange is exercised with a one-rank communicator (the
