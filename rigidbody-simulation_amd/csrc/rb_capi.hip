@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -258,6 +259,38 @@ struct rb_world {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
     double t_sum_ms = 0;
     int64_t t_n = 0;
+
+    // cell-ordered tile form (rb_tiles.hip): sphere worlds on
+    // one rank step in tile slots when eligible (tile_eligible).  The bins
+    // (the state sorted by column, per step parity) are a cache of the
+    // id-ordered state rows and snapshot: built from them at the first tile
+    // run, carried from run to run, written back at the end of each run by
+    // the unbin kernel — only if no step of it raised ERR_TILE, so that a
+    // failed run leaves the id-ordered state at the start of the first
+    // failed run, which the host replays with the hashed-cell forms
+    // (tile_finish) at the next sync point.
+    int tile_mode = 0;             // RBHIP_TILE: 0 off (default until it beats the hashed forms), 1 every eligible world, -1 auto (>= tile_min_bodies)
+    int32_t tile_ntypes = 0;       // distinct (m, I) of the bodies when <= TILE_TYPES (else 0: no tile form)
+    double tile_type_val[TILE_TYPES][4] = {};   // m ix iy iz of each type
+    uint8_t *tile_type_of = nullptr;   // [N]
+    int64_t tile_min_bodies = 16385;
+    int32_t tile_tc = 0, tile_ntx = 0, tile_nty = 0, tile_cap = TILE_THREADS;
+    bool tile_fit_valid = false;
+    int tile_valid_sp = -1;        // the bins of this parity hold the state at step c (-1: no bins)
+    void *tile_mem = nullptr;      // bins x 2 (column tables, positions, ids, state), far lists x 2
+    size_t tile_mem_bytes = 0;
+    int32_t *tile_fill = nullptr;  // build scratch [slots][TILE_OFFW]
+    uint32_t *tile_gen = nullptr;  // [2] generation of each parity's bins (far-list tags)
+    int32_t *tile_why = nullptr;   // TILE_WHY_* bits raised (device)
+    unsigned long long *tile_commits = nullptr;   // runs committed by the unbin kernel (device)
+    int64_t *tile_host = nullptr;  // pinned: err, why, commits
+    unsigned long long tile_commits_seen = 0;
+    struct TileRun { int64_t c0, n; double dt, e, mu, thr; };
+    std::vector<TileRun> tile_pending;    // runs enqueued since the last check
+    int64_t tile_stats[4] = {};    // runs, steps committed, runs rolled back, bin builds
+    int32_t tile_why_seen = 0;     // why bits of the runs rolled back (OR)
+    int32_t tile_backoff = 0, tile_skip = 0;   // eligible runs to step hashed after a roll-back (doubling)
+    bool tile_replaying = false;   // tile_finish's replay steps hashed
 
     int sp() const { return (int)(c % 2); }
 };
@@ -600,8 +633,9 @@ int gen_guard(rb_world *w, int64_t nsteps) {
 
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded = false);
 
-// every run that awaits its check at the next sync point
-int finish_pending(rb_world *) { return RB_OK; }
+// every run that awaits its check at the next sync point (tile runs)
+int tile_finish(rb_world *w);
+int finish_pending(rb_world *w) { return tile_finish(w); }
 
 // Guarded chunks (enqueue_steps): the chunk-start copy (state rows,
 // snapshot, box orientations, error word), the check after the chunk (error
@@ -645,6 +679,7 @@ int chunk_restore(rb_world *w) {
     HIPCHK(hipMemcpyAsync(w->err, o + st + 2 * sn, sizeof(int32_t), hipMemcpyDeviceToDevice, w->stream));
     if (w->boxes) HIPCHK(hipMemsetAsync(w->defer_cnt, 0, sizeof(int32_t) * 2, w->stream));
     w->primed = false;
+    w->tile_valid_sp = -1;
     return RB_OK;
 }
 // twice the buckets (both tables, emptied), if under the world's limit; the
@@ -844,6 +879,288 @@ inline void best_period_split(const std::vector<PeriodSet> &sets, const double n
         }
 }
 
+// ---- the cell-ordered tile form (rb_tiles.hip) -----------------
+bool tile_eligible(const rb_world *w) {
+    if (w->tile_mode == 0 || w->tile_replaying || w->P != 1 || !w->all_spheres || w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
+        return false;
+    // (more than TILE_TYPES distinct (m, I): the hashed forms, which read them by id)
+    if (w->maxp > 32 || w->n_local <= 0 || w->N > (int64_t)TILE_ID_MASK + 1 || w->tile_ntypes < 1) return false;
+    return w->tile_mode == 1 || w->n_local >= w->tile_min_bodies;
+}
+
+// The tile grid from body positions (x, y at pos[k * stride], pos[k * stride + 1]):
+// columns of the hashed cell size; tc columns per tile edge so that a tile
+// holds ~80 bodies on average (a slot steps at most TILE_THREADS) and none
+// holds more than 7/8 of that limit at the fit; ntx x nty slots covering the
+// scene's extent plus a margin (periodic: a scene that outgrows it folds
+// onto itself, which stays exact).
+void tile_fit(rb_world *w, const double *pos, int64_t stride) {
+    const double inv = w->inv_cs;
+    std::vector<int64_t> cols;
+    cols.reserve((size_t)w->N);
+    int64_t lo[2] = {INT64_MAX, INT64_MAX}, hi[2] = {INT64_MIN, INT64_MIN};
+    for (int64_t b = 0; b < w->N; ++b) {
+        const double fx = pos[b * stride] * inv, fy = pos[b * stride + 1] * inv;
+        if (!(fabs(fx) < 1e9 && fabs(fy) < 1e9)) continue;
+        const int64_t cx = (int64_t)floor(fx), cy = (int64_t)floor(fy);
+        lo[0] = std::min(lo[0], cx); hi[0] = std::max(hi[0], cx);
+        lo[1] = std::min(lo[1], cy); hi[1] = std::max(hi[1], cy);
+        cols.push_back(((cx + (1 << 30)) << 31) | (cy + (1 << 30)));
+    }
+    if (cols.empty()) { lo[0] = lo[1] = 0; hi[0] = hi[1] = 0; }
+    std::sort(cols.begin(), cols.end());
+    const int64_t nocc = std::max<int64_t>(1, (int64_t)(std::unique(cols.begin(), cols.end()) - cols.begin()));
+    const double per_col = (double)std::max<int64_t>(1, (int64_t)cols.size()) / (double)nocc;
+    int tc = (int)lround(sqrt(80.0 / per_col));
+    tc = std::max(TILE_TC_MIN, std::min(TILE_TC_MAX, tc));
+    if (const char *ev = getenv("RBHIP_TILE_COLS")) tc = std::max(TILE_TC_MIN, std::min(TILE_TC_MAX, atoi(ev)));
+    // the densest tile at this fit under 3/4 of a slot's limit
+    for (; tc > TILE_TC_MIN; --tc) {
+        std::vector<int64_t> t;
+        t.reserve(cols.size());
+        for (int64_t b = 0; b < w->N; ++b) {
+            const double fx = pos[b * stride] * inv, fy = pos[b * stride + 1] * inv;
+            if (!(fabs(fx) < 1e9 && fabs(fy) < 1e9)) continue;
+            const int64_t tx = (int64_t)floor(floor(fx) / tc), ty = (int64_t)floor(floor(fy) / tc);
+            t.push_back(((tx + (1 << 30)) << 31) | (ty + (1 << 30)));
+        }
+        std::sort(t.begin(), t.end());
+        int64_t worst = 0;
+        for (size_t a = 0; a < t.size();) {
+            size_t e = a;
+            while (e < t.size() && t[e] == t[a]) ++e;
+            worst = std::max<int64_t>(worst, (int64_t)(e - a));
+            a = e;
+        }
+        if (worst <= 7 * TILE_THREADS / 8) break;
+    }
+    int64_t ntx = (hi[0] - lo[0]) / tc + 3, nty = (hi[1] - lo[1]) / tc + 3;
+    // a scene spread far (outliers): fold instead of launching empty slots
+    const int64_t max_slots = 4 * ((w->N + 23) / 24) + 64;
+    while (ntx * nty > max_slots) {
+        if (ntx >= nty) ntx = (ntx + 1) / 2; else nty = (nty + 1) / 2;
+    }
+    w->tile_tc = tc;
+    w->tile_ntx = (int32_t)std::max<int64_t>(3, ntx);
+    w->tile_nty = (int32_t)std::max<int64_t>(3, nty);
+    w->tile_fit_valid = true;
+}
+
+size_t tile_bins_bytes(const rb_world *w) {
+    const size_t slots = (size_t)w->tile_ntx * w->tile_nty, cap = (size_t)w->tile_cap, esz = (size_t)w->esz;
+    return slots * TILE_OFFW * 4 + slots * cap * (4 * esz + 4 + TILE_STW * esz) + 256 +
+           (size_t)TILE_FARMAX * (4 * esz + 4 + TILE_STW * esz) + 256;
+}
+template <typename T> TileBins<T> tile_bins(const rb_world *w, int sp) {
+    const size_t slots = (size_t)w->tile_ntx * w->tile_nty, cap = (size_t)w->tile_cap;
+    char *b = static_cast<char *>(w->tile_mem) + (size_t)sp * tile_bins_bytes(w);
+    TileBins<T> t;
+    t.off = reinterpret_cast<int32_t *>(b);
+    b += slots * TILE_OFFW * 4;
+    t.pos = reinterpret_cast<Snap<T> *>(b);
+    b += slots * cap * 4 * sizeof(T);
+    t.st = reinterpret_cast<T *>(b);
+    b += slots * cap * TILE_STW * sizeof(T);
+    t.id = reinterpret_cast<int32_t *>(b);
+    b += (slots * cap * 4 + 255) / 256 * 256;
+    t.far_hdr = reinterpret_cast<unsigned long long *>(b);
+    b += 256;
+    t.far_pos = reinterpret_cast<Snap<T> *>(b);
+    b += (size_t)TILE_FARMAX * 4 * sizeof(T);
+    t.far_st = reinterpret_cast<T *>(b);
+    b += (size_t)TILE_FARMAX * TILE_STW * sizeof(T);
+    t.far_id = reinterpret_cast<int32_t *>(b);
+    return t;
+}
+
+int tile_alloc(rb_world *w) {
+    const size_t need = 2 * tile_bins_bytes(w);
+    const size_t slots = (size_t)w->tile_ntx * w->tile_nty;
+    if (w->tile_mem && w->tile_mem_bytes >= need && w->tile_fill) {
+        // the fill scratch is sized for the slots too
+        return RB_OK;
+    }
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);                                  // captured bin pointers
+    if (w->tile_mem) { HIPCHK(hipFree(w->tile_mem)); w->tile_mem = nullptr; }
+    if (w->tile_fill) { HIPCHK(hipFree(w->tile_fill)); w->tile_fill = nullptr; }
+    HIPCHK(hipMalloc(&w->tile_mem, need));
+    HIPCHK(hipMalloc((void **)&w->tile_fill, slots * TILE_OFFW * 4));
+    w->tile_mem_bytes = need;
+    if (!w->tile_gen) {
+        HIPCHK(hipMalloc((void **)&w->tile_gen, 2 * sizeof(uint32_t)));
+        HIPCHK(hipMalloc((void **)&w->tile_why, sizeof(int32_t)));
+        HIPCHK(hipMalloc((void **)&w->tile_commits, sizeof(unsigned long long)));
+        HIPCHK(hipMemset(w->tile_why, 0, sizeof(int32_t)));
+        HIPCHK(hipMemset(w->tile_commits, 0, sizeof(unsigned long long)));
+        HIPCHK(hipHostMalloc((void **)&w->tile_host, 4 * sizeof(int64_t), 0));
+        w->tile_commits_seen = 0;
+    }
+    return RB_OK;
+}
+
+template <typename T> TileIO<T> make_tile_io(rb_world *w, int64_t c) {
+    TileIO<T> p{};
+    const int sp = (int)(c % 2);
+    p.bins = tile_bins<T>(w, sp);
+    p.gen = w->tile_gen + sp;
+    p.snap = dp<Snap<T>>(w->snap[sp], 0);
+    p.st = BodyState<T>{dp<T>(w->state, 0), w->S};
+    p.fill = w->tile_fill;
+    p.type_of = w->tile_type_of;
+    p.tc = w->tile_tc; p.ntx = w->tile_ntx; p.nty = w->tile_nty; p.cap = w->tile_cap;
+    p.inv_col = (T)w->inv_cs;
+    p.n = w->N;
+    p.err = w->err;
+    p.why = w->tile_why;
+    p.commits = w->tile_commits;
+    return p;
+}
+
+template <typename T> TileParams<T> make_tile_step(rb_world *w, int64_t c, double dt, double e, double mu, double thr) {
+    TileParams<T> p{};
+    const int sp = (int)(c % 2);
+    p.cur = tile_bins<T>(w, sp);
+    p.next = tile_bins<T>(w, 1 - sp);
+    p.gen_cur = w->tile_gen + sp;
+    p.gen_next = w->tile_gen + (1 - sp);
+    p.sp = make_step<T>(w, c, dt, e, mu, thr, false);
+    p.ntypes = w->tile_ntypes;
+    for (int t = 0; t < w->tile_ntypes; ++t)
+        for (int k = 0; k < 4; ++k) p.types[t][k] = (T)w->tile_type_val[t][k];
+    p.tc = w->tile_tc; p.ntx = w->tile_ntx; p.nty = w->tile_nty; p.cap = w->tile_cap;
+    p.inv_col = (T)w->inv_cs;
+    p.why = w->tile_why;
+    return p;
+}
+
+// the bins of step c from the id-ordered state (snapshot and state rows)
+int tile_build(rb_world *w) {
+    if (!w->tile_fit_valid) {
+        // positions: the staging when it mirrors the state, else the snapshot
+        if (w->io_q_h && w->mirror_version == w->state_version) {
+            tile_fit(w, w->io_q_h, 7);
+        } else {
+            std::vector<double> q((size_t)4 * w->N);
+            if (w->dtype == RB_F64) {
+                HIPCHK(hipMemcpyAsync(q.data(), w->snap[w->sp()], sizeof(double) * q.size(), hipMemcpyDeviceToHost, w->stream));
+                HIPCHK(hipStreamSynchronize(w->stream));
+            } else {
+                std::vector<float> f(q.size());
+                HIPCHK(hipMemcpyAsync(f.data(), w->snap[w->sp()], sizeof(float) * f.size(), hipMemcpyDeviceToHost, w->stream));
+                HIPCHK(hipStreamSynchronize(w->stream));
+                for (size_t k = 0; k < f.size(); ++k) q[k] = f[k];
+            }
+            tile_fit(w, q.data(), 4);
+        }
+        drop_graphs(w);                              // the grid is a captured kernel argument
+    }
+    if (int rc = tile_alloc(w)) return rc;
+    const int sp = w->sp();
+    const size_t slots = (size_t)w->tile_ntx * w->tile_nty;
+    HIPCHK(hipMemsetAsync(w->tile_fill, 0, slots * TILE_OFFW * 4, w->stream));
+    for (int k = 0; k < 2; ++k) {
+        // far lists empty (tag 0: never a live generation)
+        HIPCHK(hipMemsetAsync(w->dtype == RB_F64 ? (void *)tile_bins<double>(w, k).far_hdr : (void *)tile_bins<float>(w, k).far_hdr,
+                              0, sizeof(unsigned long long), w->stream));
+    }
+    HIPCHK(hipMemsetAsync(w->dtype == RB_F64 ? (void *)tile_bins<double>(w, sp).off : (void *)tile_bins<float>(w, sp).off, 0,
+                          slots * TILE_OFFW * 4, w->stream));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(w->tile_gen + sp), 1, 1, w->stream));
+    HIPCHK(w->dtype == RB_F64 ? launch_tile_build<double>(make_tile_io<double>(w, w->c), w->stream)
+                              : launch_tile_build<float>(make_tile_io<float>(w, w->c), w->stream));
+    w->tile_valid_sp = sp;
+    w->tile_stats[3] += 1;
+    return RB_OK;
+}
+
+// One run of n tile steps from step c (graph-replayed in chunks; the last
+// chunk ends with the unbin kernel), recorded as pending until checked.
+int tile_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
+    if (w->tile_valid_sp != w->sp()) {
+        if (int rc = finish_pending(w)) return rc;  // (the build reads the id-ordered state)
+        if (int rc = tile_build(w)) return rc;
+    }
+    const bool f64 = w->dtype == RB_F64;
+    const int64_t c0 = w->c, chunk_max = 512;
+    int64_t left = n;
+    while (left > 0) {
+        const int64_t K = left > chunk_max ? chunk_max : left;
+        const bool last = K == left;
+        const int variant = 16 | (int)w->record | (last ? 32 : 0);
+        int rc = graph_replay(w, K, variant, dt, e, mu, thr, [&](hipStream_t s, int64_t cs) {
+            for (int64_t k = 0; k < K; ++k) {
+                const hipError_t r = f64 ? launch_tile_step<double>(make_tile_step<double>(w, cs + k, dt, e, mu, thr), w->maxp, s)
+                                         : launch_tile_step<float>(make_tile_step<float>(w, cs + k, dt, e, mu, thr), w->maxp, s);
+                HIPCHK(r);
+            }
+            if (last) HIPCHK(f64 ? launch_tile_unbin<double>(make_tile_io<double>(w, cs + K), s)
+                                 : launch_tile_unbin<float>(make_tile_io<float>(w, cs + K), s));
+            return (int)RB_OK;
+        });
+        if (rc) return rc;
+        w->c += K;
+        left -= K;
+    }
+    w->tile_valid_sp = w->sp();
+    w->primed = false;                               // the hashed forms' table is stale
+    w->tile_pending.push_back(rb_world::TileRun{c0, n, dt, e, mu, thr});
+    w->tile_stats[0] += 1;
+    return RB_OK;
+}
+
+// The check of the pending tile runs: every run whose unbin committed is
+// done; the first run that raised ERR_TILE and every run after it are
+// replayed, from the id-ordered state (which still holds that run's start),
+// by the hashed-cell forms — which report any real error themselves.
+int tile_finish(rb_world *w) {
+    if (w->tile_pending.empty()) return RB_OK;
+    HIPCHK(hipMemcpyAsync(w->tile_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipMemcpyAsync(w->tile_host + 1, w->tile_why, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipMemcpyAsync(w->tile_host + 2, w->tile_commits, sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    const int32_t err = (int32_t)reinterpret_cast<int32_t *>(w->tile_host)[0];
+    const int32_t why = (int32_t)reinterpret_cast<int32_t *>(w->tile_host + 1)[0];
+    const unsigned long long commits = (unsigned long long)w->tile_host[2];
+    const size_t ok = (size_t)(commits - w->tile_commits_seen);
+    w->tile_commits_seen = commits;
+    std::vector<rb_world::TileRun> runs;
+    runs.swap(w->tile_pending);
+    for (size_t k = 0; k < ok && k < runs.size(); ++k) w->tile_stats[1] += runs[k].n;
+    if (!(err & ERR_TILE)) {
+        if (w->tile_backoff > 0) w->tile_backoff /= 2;
+        return RB_OK;
+    }
+    // roll back to the start of the first failed run and replay it and
+    // every later one with the hashed-cell forms (guarded chunks: the
+    // replay grows max_partners or refits the table as a synchronous
+    // rb_step would)
+    w->tile_stats[2] += 1;
+    w->tile_why_seen |= why;
+    const int32_t clean = err & ~ERR_TILE;
+    HIPCHK(hipMemcpyAsync(w->err, &clean, sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
+    HIPCHK(hipMemsetAsync(w->tile_why, 0, sizeof(int32_t), w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    w->tile_valid_sp = -1;
+    w->primed = false;
+    if (why & (TILE_WHY_CAP | TILE_WHY_WINDOW)) w->tile_fit_valid = false;   // the scene outgrew the fit
+    w->tile_backoff = w->tile_backoff ? std::min(2 * w->tile_backoff, 64) : 1;
+    w->tile_skip = w->tile_backoff;
+    const size_t first = std::min(ok, runs.size());
+    w->c = first < runs.size() ? runs[first].c0 : w->c;
+    const bool saved = w->sync_call;
+    w->sync_call = true;
+    w->tile_replaying = true;
+    int rc = RB_OK;
+    for (size_t k = first; k < runs.size() && !rc; ++k) {
+        const rb_world::TileRun &r = runs[k];
+        rc = enqueue_steps(w, r.n, r.dt, r.e, r.mu, r.thr, false);
+    }
+    w->tile_replaying = false;
+    w->sync_call = saved;
+    return rc;
+}
+
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
@@ -854,8 +1171,20 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
     HIPCHK(hipSetDevice(w->device));
+    // the tile form for runs of >= 2 steps, or to continue from its bins;
+    // pending tile runs chain (their check waits for the next sync point),
+    // anything else first settles them
+    const bool tile = !sharded && tile_eligible(w) && (nsteps >= 2 || w->tile_valid_sp == w->sp()) &&
+                      w->tile_pending.size() < 256;
+    if (tile && w->tile_skip > 0 && w->tile_valid_sp != w->sp()) {
+        --w->tile_skip;                              // (back-off after a roll-back: this run steps hashed)
+    } else if (tile) {
+        w->state_version += 1;
+        return tile_run(w, nsteps, dt, e, mu, thr);
+    }
     if (int rc = finish_pending(w)) return rc;
     w->state_version += 1;
+    w->tile_valid_sp = -1;                           // the hashed forms advance the id-ordered state
     if (int rc = gen_guard(w, nsteps)) return rc;
     if (!w->primed || (w->law == RB_LAW_BALLS && (dt != w->prm_dt || e != w->prm_e || mu != w->prm_mu))) {
         int rc = prime(w, dt, e, mu);
@@ -1117,6 +1446,27 @@ int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &boun
     w->inv_cs = 1.0 / cs;
     for (int64_t b = 0; b < w->N; ++b) w->all_spheres = w->all_spheres && d->kind[b] == RB_BODY_SPHERE;
     HIPCHK(hipMemcpy(w->consts, c.data(), sizeof(T) * c.size(), hipMemcpyHostToDevice));
+    // the tile form's constant types: the distinct (m, I) of the bodies, as
+    // the arithmetic type holds them (a record carries its type, so the tile
+    // kernel reads m and I from a table in LDS instead of by body id)
+    {
+        std::vector<std::array<T, 4>> types;
+        std::vector<uint8_t> type_of((size_t)w->N, 0);
+        for (int64_t b = 0; b < w->N && types.size() <= (size_t)TILE_TYPES; ++b) {
+            const std::array<T, 4> t = {(T)d->mass[b], (T)d->inertia[3 * b], (T)d->inertia[3 * b + 1], (T)d->inertia[3 * b + 2]};
+            size_t k = 0;
+            while (k < types.size() && memcmp(types[k].data(), t.data(), sizeof(t)) != 0) ++k;
+            if (k == types.size()) types.push_back(t);
+            type_of[(size_t)b] = (uint8_t)k;
+        }
+        if (types.size() <= (size_t)TILE_TYPES) {
+            for (size_t t = 0; t < types.size(); ++t)
+                for (int k = 0; k < 4; ++k) w->tile_type_val[t][k] = (double)types[t][k];
+            HIPCHK(hipMalloc((void **)&w->tile_type_of, (size_t)w->N));
+            HIPCHK(hipMemcpy(w->tile_type_of, type_of.data(), (size_t)w->N, hipMemcpyHostToDevice));
+            w->tile_ntypes = (int32_t)types.size();
+        }
+    }
     std::vector<int32_t> k((size_t)w->Npad, 0);
     for (int64_t b = 0; b < w->N; ++b) k[(size_t)b] = d->kind[b];
     HIPCHK(hipMemcpy(w->kind, k.data(), sizeof(int32_t) * k.size(), hipMemcpyHostToDevice));
@@ -1134,6 +1484,10 @@ void free_world(rb_world *w) {
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (w->opt_save) (void)hipFree(w->opt_save);
+    void *tbufs[] = {w->tile_mem, w->tile_fill, w->tile_gen, w->tile_why, w->tile_commits, w->tile_type_of};
+    for (void *b : tbufs)
+        if (b) (void)hipFree(b);
+    if (w->tile_host) (void)hipHostFree(w->tile_host);
     if (w->defer_host) (void)hipHostFree(w->defer_host);
     if (w->io_q_h) (void)hipHostFree(w->io_q_h);
     if (w->io_v_h) (void)hipHostFree(w->io_v_h);
@@ -1217,6 +1571,12 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_WIDE_MAX_BODIES")) w->wide_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_HELP")) w->wide_help = atoi(ev) != 0;
+    // the cell-ordered tile form (rb_tiles.hip): RBHIP_TILE = 0 off, 1 every
+    // eligible world, -1 auto (eligible worlds of >= RBHIP_TILE_MIN_BODIES
+    // bodies); off by default while it measures slower than the hashed forms
+    // on C2/C3
+    if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
+    if (const char *ev = getenv("RBHIP_TILE_MIN_BODIES")) w->tile_min_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
@@ -1474,6 +1834,8 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
                                             : launch_state_in<float>(make_io<float>(w), w->stream);
     HIPCHK(e);
     w->primed = false;
+    w->tile_valid_sp = -1;
+    w->tile_fit_valid = false;                           // (refitted at the next tile run)
     w->state_version += 1;
     // uploading the staging's bytes yields exactly this state (one rank)
     w->mirror_version = w->P == 1 ? w->state_version : -1;
@@ -1926,6 +2288,7 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
     w->law = law;
     w->tol = tol;
     w->state_version += 1;
+    w->tile_valid_sp = -1;
     // cell = 2 x the largest reach: 2 x 2 rmax, or 2 x (2 rmax + tol)
     const double reach = law == RB_LAW_BALLS ? 2.0 * w->rmax + tol : 2.0 * w->rmax;
     w->inv_cs = 1.0 / (reach > 0 ? 2.0 * reach * 1.001 : 1.0);
@@ -1943,10 +2306,13 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
-    const int form = step_form(w);
+    const bool tile = tile_eligible(w);
+    const int form = tile ? FORM_TILE : step_form(w);
     const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), form, w->box_stats[0], w->box_stats[1], w->refits,
                                        w->table_grows, w->H, (int64_t)w->maxp, w->io_stats[0], w->io_stats[1],
-                                       0, 0, 0, 0, 0, 0, 0, 0};
+                                       w->tile_stats[0], w->tile_stats[1], w->tile_stats[2], w->tile_stats[3],
+                                       (int64_t)w->tile_why_seen, (int64_t)w->tile_ntx * w->tile_nty,
+                                       (int64_t)w->tile_tc, tile && w->tile_skip == 0 ? 1 : 0};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

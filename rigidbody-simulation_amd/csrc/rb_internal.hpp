@@ -256,10 +256,86 @@ template <typename T> struct HaloParams {
     T *quat;
 };
 
+// ---- the cell-ordered tile form (rb_tiles.hip) -------------------
+// Sphere worlds on one rank.  The ground plane (x, y) is cut into columns of
+// the hashed forms' cell size (2 x the largest contact reach, so every
+// partner of a body lies in the 2 x 2 nearest columns) and the columns into
+// square tiles of tc x tc.  Tiles map periodically onto ntx x nty slots;
+// one workgroup steps one slot.  Each slot keeps a BIN per step parity: the
+// full state of every body the slot stepped, in the column order of the
+// slot's tile extended by one ring of columns ((tc + 2)^2 columns, row-major
+// from (-1, -1)): a body that left the tile by at most one column lies in
+// the ring, i.e. in a neighbouring tile's interior, and that neighbour
+// takes it over at the next step.  A step reads the 3 x 3 neighbouring bins
+// with coalesced loads, sorts the window of columns (tc + 2)^2 in LDS
+// (counts known from the bins' column tables before a record is loaded),
+// searches, solves and integrates its own bodies, and writes its next bin
+// sorted by column: no atomics on the common path.  A body that moved more
+// than a column goes to a small FAR list (one atomic per such body) that
+// every slot scans.  Anything the form cannot take (a full bin or window,
+// a full far list, too many partners, a bad position) raises ERR_TILE: the
+// host rolls the run back and replays it with the hashed-cell forms, which
+// also report any real error.
+constexpr int32_t ERR_TILE = 1 << 22;
+enum : int32_t { TILE_WHY_CAP = 1, TILE_WHY_WINDOW = 2, TILE_WHY_FAR = 4, TILE_WHY_PARTNERS = 8, TILE_WHY_DOMAIN = 16 };
+constexpr int TILE_THREADS = 128;        // workgroup size; also the most bodies a slot steps
+constexpr int TILE_TC_MIN = 4, TILE_TC_MAX = 8;
+constexpr int TILE_OFFW = 128;           // int32 words per bin's column table (>= (tc + 2)^2 + 1)
+constexpr int TILE_WMAX = 384;           // window records a workgroup holds in LDS
+constexpr int TILE_FARMAX = 1024;        // far-list capacity
+constexpr int TILE_FARWIN = 32;          // far bodies one window holds
+constexpr int TILE_STW = 10;             // state reals per record: q (w x y z), v, w
+// a record's id word: the body id, and in the top bits its constants' type
+// (worlds whose bodies share at most TILE_TYPES distinct (m, I): the kernel
+// selects them from its arguments — no memory access between the record's
+// arrival and the body's first arithmetic — instead of gathering by id)
+constexpr int TILE_ID_BITS = 26;
+constexpr int32_t TILE_ID_MASK = (1 << TILE_ID_BITS) - 1;
+constexpr int TILE_TYPES = 4;
+template <typename T> struct TileBins {
+    int32_t *off;                        // [slots][TILE_OFFW] column c at [off[c], off[c + 1]); off[ncol] = count
+    Snap<T> *pos;                        // [slots][cap] x y z, bounding radius
+    int32_t *id;                         // [slots][cap] id word (id | type << TILE_ID_BITS)
+    T *st;                               // [slots][cap][TILE_STW]
+    unsigned long long *far_hdr;         // (generation << 32) | count
+    Snap<T> *far_pos;                    // [TILE_FARMAX]
+    int32_t *far_id;
+    T *far_st;                           // [TILE_FARMAX][TILE_STW]
+};
+template <typename T> struct TileParams {
+    TileBins<T> cur, next;
+    const uint32_t *gen_cur;             // this step's generation (far-list tags)
+    uint32_t *gen_next;                  // written by block 0: gen + 1
+    StepParams<T> sp;                    // the physics fields (planes, g, dt, e, mu, thr, oriented, recording,
+                                         // err, cs): the same per-body code as the hashed forms (rb_body.hpp)
+    T types[TILE_TYPES][4];              // m, ix, iy, iz of each constant type (1..TILE_TYPES)
+    int32_t ntypes;
+    int32_t tc, ntx, nty, cap;
+    T inv_col;                           // 1 / column width
+    int32_t *why;                        // TILE_WHY_* bits (diagnostics)
+};
+// bins <-> the id-ordered state (rb_set_state / rb_get_state / the hashed forms)
+template <typename T> struct TileIO {
+    TileBins<T> bins;                    // the bins of the current step parity
+    const uint32_t *gen;                 // their generation
+    Snap<T> *snap;                       // [Npad] the id-ordered snapshot of the same step
+    BodyState<T> st;
+    const uint8_t *type_of;              // [N] constants' type per body (nullptr: type 0)
+    int32_t *fill;                       // [slots][TILE_OFFW] scratch (build)
+    int32_t tc, ntx, nty, cap;
+    T inv_col;
+    int64_t n;
+    int32_t *err, *why;
+    unsigned long long *commits;         // unbin: runs committed (the host compares)
+};
+template <typename T> hipError_t launch_tile_step(const TileParams<T> &p, int maxp, hipStream_t s);
+template <typename T> hipError_t launch_tile_build(const TileIO<T> &p, hipStream_t s);   // bins zeroed by the caller
+template <typename T> hipError_t launch_tile_unbin(const TileIO<T> &p, hipStream_t s);
+
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one
 // lane per body at one wave per SIMD (mid-size scenes)
-enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4 };
+enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4, FORM_TILE = 5 };
 // boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
 // the wide form's kernel alone (its own translation unit: scheduled for memory clauses)

@@ -54,6 +54,7 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][16];
 #include "rb_boxes.hpp"
 #include "rb_grid.hpp"
 #include "rb_internal.hpp"
+#include "rb_body.hpp"
 
 // diagnostic builds only (scripts/ablate.py): 1 = skip the sphere-sphere
 // broadphase, 2 = skip the world-inertia inverse (identity), 3 = empty
@@ -71,53 +72,6 @@ __global__ __launch_bounds__(256) void insert_kernel(InsertParams<T> p) {
     const int64_t id = p.first + k;
     if (id >= p.skip_lo && id < p.skip_hi) return;
     insert_id(p.grid, p.tab, p.err, p.snap[id], (uint32_t)id | (p.kind[id] != 0 ? BOX_FLAG : 0u), *p.tab.gen);
-}
-
-template <typename T>
-__device__ __forceinline__ void record(const StepParams<T> &p, int32_t l, int32_t &nrec, int32_t partner,
-                                       int32_t kind, T dist) {
-    if (!p.rec_count) return;
-    if (nrec < p.maxrec) {
-        const int64_t o = (int64_t)l * p.maxrec + nrec;
-        p.rec_partner[o] = partner;
-        p.rec_kind[o] = kind;
-        p.rec_dist[o] = dist;
-    }
-    ++nrec;
-}
-
-// Lazily evaluated inv(inertia_world): the reference computes it every step
-// (collision.py:62) but it only reaches the state through a torque or an
-// applied impulse; computing it on first use is value-identical and keeps
-// it out of the broadphase's register live range.
-template <typename T> struct LazyInvI {
-    V3<T> I;
-    Q4<T> q;
-    bool have = false;
-    M3<T> m;
-    __device__ __forceinline__ const M3<T> &get() {
-        if (!have) {
-#if RB_ABLATE == 2
-            for (int k = 0; k < 9; ++k) m.a[k] = (k % 4 == 0) ? T(1) / I.x : T(0);
-#else
-            m = np_inv3(inertia_world(I, q));
-#endif
-            have = true;
-        }
-        return m;
-    }
-};
-
-// one contact of body i through the reference's skip rules then K2
-template <typename T>
-__device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Contact<T> &con, V3<T> x, V3<T> n,
-                                              T m, T k, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
-    if (!(con.dist < T(0))) return;                 // collision.py:74 (NaN fails too)
-    if (absval(con.dist) < p.thr) return;           // collision.py:79-80
-    const V3<T> r = {con.pos.x - x.x, con.pos.y - x.y, con.pos.z - x.z};   // :75
-    T jn;
-    V3<T> jt;
-    if (impulse(k, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
 }
 
 // Candidate test shared by every search form: true if the candidate with
@@ -351,20 +305,6 @@ template <typename T> struct Lead {
 #ifndef RB_SOLVE_DEPTH
 #define RB_SOLVE_DEPTH 1
 #endif
-
-// a4 (collision.py:66-70): gravity plus the optional applied force / torque
-template <typename T>
-__device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T m, LazyInvI<T> &invI, V3<T> &v,
-                                            V3<T> &w) {
-    V3<T> F = {m * p.g[0], m * p.g[1], m * p.g[2]};
-    if (p.xfrc) F = {p.xfrc[l] + F.x, p.xfrc[p.S + l] + F.y, p.xfrc[2 * p.S + l] + F.z};
-    v = {v.x + (F.x / m) * p.dt, v.y + (F.y / m) * p.dt, v.z + (F.z / m) * p.dt};
-    if (p.xfrc) {
-        const V3<T> tdt = {p.xfrc[3 * p.S + l] * p.dt, p.xfrc[4 * p.S + l] * p.dt, p.xfrc[5 * p.S + l] * p.dt};
-        const V3<T> dw = np_matvec(invI.get(), tdt);
-        w = {w.x + dw.x, w.y + dw.y, w.z + dw.z};
-    }
-}
 
 // Everything after the contact search for one body (lane): gravity (unless
 // already applied: forced), the Gauss-Seidel solves in canonical order,
