@@ -54,7 +54,9 @@ this run loaded (the file records its hash).
 cpu_baseline (rank 0, N = 1): the oracle (C restatement of the reference
 arithmetic) over the full single-GPU scene for --cpu-steps steps from t = 0,
 on the host-core share (OMP_NUM_THREADS if set, else the affinity mask) and
-on one core, with the host's nproc / affinity / CPU model.  `accuracy`: the
+on one core, with the host's nproc / affinity / CPU model; `reference_loop`
+quotes the reference's own Python loop on C2 (scripts/reference_loop.py,
+committed JSON profiles/r05/reference_loop_c2.json).  `accuracy`: the
 GPU state after the same --cpu-steps steps against that oracle run (BASELINE
 metric "CPU-ref max|Δpos|"), and whether the last step's contact lists agree.
 """
@@ -162,7 +164,30 @@ def cpu_baseline(cfg: str, steps: int):
                       f"multi_sphere_bounce.py arithmetic, bit-identical to the GPU path) on the full {cfg} "
                       f"scene, {sc.n} bodies x {steps} steps from t=0: {cores} OpenMP threads "
                       f"{rates[cores][1]:.1f} s, 1 thread {rates[1][1]:.1f} s"}
+    ref_loop = reference_loop_quote()
+    if ref_loop:
+        base["reference_loop"] = ref_loop
     return base, ref
+
+
+REFERENCE_LOOP = os.path.join("profiles", "r05", "reference_loop_c2.json")
+
+
+def reference_loop_quote():
+    """The reference's own Python step loop timed in the build container
+    (scripts/reference_loop.py; the reference cannot travel to the GPU box),
+    quoted from the committed JSON with its source file."""
+    path = os.path.join(ROOT, REFERENCE_LOOP)
+    try:
+        with open(path) as f:
+            r = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {"value": r["body_steps_per_s"], "unit": "body-steps/s", "cores": r["cores"],
+            "value_excluding_mj_forward": r["body_steps_per_s_excluding_mj_forward"],
+            "config": r["config"], "bodies": r["bodies"], "steps": r["steps"],
+            "cpu_model": r["cpu_model"], "nproc": r["nproc"], "source": REFERENCE_LOOP,
+            "script": r["script"], "measured_on": "build container (not the GPU box)"}
 
 
 def _pairs(cnt, par):
