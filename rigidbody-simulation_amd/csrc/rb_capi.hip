@@ -35,55 +35,72 @@
 
 // Threads.  A graph capture on one thread's stream is invalidated by a
 // null-stream or device-wide call (hipMalloc, hipMemset, hipMemcpy, hipFree,
-// ...) that another thread makes meanwhile, and that call fails too (seen
-// with two threads creating, stepping and destroying their own worlds).  So
-// every entry point runs inside an ApiScope, and a capture (graph_replay)
-// inside a CaptureScope: a capture starts once no other thread is inside an
-// entry point (other than capturing too), and no entry point starts while a
-// capture runs.  Captures of several threads may overlap.
+// ...) that another thread makes on the same device meanwhile, and that call
+// fails too (seen with two threads creating, stepping and destroying their
+// own worlds).  So every entry point runs inside an ApiScope of its world's
+// device, and a capture (graph_replay) inside a CaptureScope: a capture on
+// device d starts once no other thread is inside an entry point on d (other
+// than capturing too), and no entry point on d starts while a capture on d
+// runs.  Captures of several threads may overlap; a thread working on one
+// device never waits for a capture on another.  Entry points with no device
+// (rb_comm_unique_id) or no valid world gate every device.
 namespace {
+constexpr int GATE_DEVICES = 64;
 struct Gate {
     std::mutex m;
     std::condition_variable cv;
-    int active = 0;      // threads inside an entry point, not capturing
-    int capturing = 0;   // threads inside a capture
+    int active[GATE_DEVICES] = {};      // threads inside an entry point on device d, not capturing
+    int capturing[GATE_DEVICES] = {};   // threads inside a capture on device d
+    int active_all = 0;                 // threads inside a device-less entry point
+    int capturing_any = 0;
 };
 Gate &gate() {
     static Gate g;
     return g;
 }
+int gate_dev(int d) { return d >= 0 && d < GATE_DEVICES ? d : -1; }
 thread_local int t_api_depth = 0;
+thread_local int t_api_dev = -1;
 struct ApiScope {
-    ApiScope() {
+    explicit ApiScope(int device) {
         if (t_api_depth++ == 0) {
-            std::unique_lock<std::mutex> l(gate().m);
-            gate().cv.wait(l, [] { return gate().capturing == 0; });
-            ++gate().active;
+            const int d = gate_dev(device);
+            t_api_dev = d;
+            Gate &g = gate();
+            std::unique_lock<std::mutex> l(g.m);
+            g.cv.wait(l, [&] { return d < 0 ? g.capturing_any == 0 : g.capturing[d] == 0; });
+            if (d < 0) ++g.active_all; else ++g.active[d];
         }
     }
     ~ApiScope() {
         if (--t_api_depth == 0) {
-            std::lock_guard<std::mutex> l(gate().m);
-            --gate().active;
-            gate().cv.notify_all();
+            Gate &g = gate();
+            std::lock_guard<std::mutex> l(g.m);
+            if (t_api_dev < 0) --g.active_all; else --g.active[t_api_dev];
+            g.cv.notify_all();
         }
     }
     ApiScope(const ApiScope &) = delete;
     ApiScope &operator=(const ApiScope &) = delete;
 };
-struct CaptureScope {   // (inside an ApiScope)
-    CaptureScope() {
-        std::unique_lock<std::mutex> l(gate().m);
-        --gate().active;
-        ++gate().capturing;
-        gate().cv.wait(l, [] { return gate().active == 0; });
+struct CaptureScope {   // (inside an ApiScope of a device: the capture's)
+    int d;
+    CaptureScope() : d(t_api_dev < 0 ? 0 : t_api_dev) {
+        Gate &g = gate();
+        std::unique_lock<std::mutex> l(g.m);
+        if (t_api_dev < 0) --g.active_all; else --g.active[d];
+        ++g.capturing[d];
+        ++g.capturing_any;
+        g.cv.wait(l, [&] { return g.active[d] == 0 && g.active_all == 0; });
     }
     ~CaptureScope() {
-        std::unique_lock<std::mutex> l(gate().m);
-        --gate().capturing;
-        gate().cv.notify_all();
-        gate().cv.wait(l, [] { return gate().capturing == 0; });
-        ++gate().active;
+        Gate &g = gate();
+        std::unique_lock<std::mutex> l(g.m);
+        --g.capturing[d];
+        --g.capturing_any;
+        g.cv.notify_all();
+        g.cv.wait(l, [&] { return g.capturing[d] == 0; });
+        if (t_api_dev < 0) ++g.active_all; else ++g.active[d];
     }
     CaptureScope(const CaptureScope &) = delete;
     CaptureScope &operator=(const CaptureScope &) = delete;
@@ -208,7 +225,7 @@ struct rb_world {
     int32_t *kind = nullptr;   // Npad
     void *xfrc = nullptr;      // 6 x S or null
     uint32_t *ids[2] = {};     // [H][LINE_WORDS] bucket blocks (rb_internal.hpp Table; alternate with the snapshots)
-    uint32_t *spill[2] = {};   // [2 + 2 x SPILL_CAP] ids past full buckets, per table
+    uint32_t *spill[2] = {};   // [SPILL_LINES x SPILL_LINE_WORDS] ids past full buckets, per table
     void *pos[2] = {};         // [H][LINE_WORDS] Snap<T> bucket slot snapshots
     uint32_t *gen = nullptr;   // [2] generation of the table of each step parity (rb_internal.hpp Table)
     uint32_t gen_off = 1;      // generation of step c's table = gen_off + c (host bookkeeping; only grows)
@@ -624,7 +641,7 @@ int gen_guard(rb_world *w, int64_t nsteps) {
     HIPCHK(hipStreamSynchronize(w->stream));
     for (int k = 0; k < 2; ++k) {
         HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
-        HIPCHK(hipMemset(w->spill[k], 0, sizeof(uint32_t) * 2));
+        HIPCHK(hipMemset(w->spill[k], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES));
     }
     w->gen_off = 1u - (uint32_t)w->c;   // prime() makes step c's generation 2
     w->primed = false;
@@ -1514,7 +1531,7 @@ const char *rb_last_error(void) { return g_err.c_str(); }
 const char *rb_version(void) { return "librbhip 0.2 (gfx950, HIP)"; }
 
 int rb_world_create(rb_world **out, const rb_scene_desc *d) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(d ? d->device : -1);
     if (!out || !d) return fail(RB_EINVAL, "null argument");
     *out = nullptr;
     if (d->n_bodies <= 0 || d->n_bodies > (int64_t)INT32_MAX / 2) return fail(RB_EINVAL, "n_bodies out of range");
@@ -1688,7 +1705,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     }
     for (int k = 0; k < 2; ++k) {
         ALLOC(w->ids[k], sizeof(uint32_t) * LINE_WORDS * w->H);
-        ALLOC(w->spill[k], sizeof(uint32_t) * (2 + 2 * SPILL_CAP));
+        ALLOC(w->spill[k], sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES);
         // slot snapshots feed the cooperative search only
         if (needs_slot_snapshots(coop, split)) ALLOC(w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * w->H);
     }
@@ -1705,8 +1722,8 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         // bucket headers of generation 0: every table's generation is >= 2
         hipMemset(w->ids[0], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
         hipMemset(w->ids[1], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
-        hipMemset(w->spill[0], 0, sizeof(uint32_t) * 2) != hipSuccess ||
-        hipMemset(w->spill[1], 0, sizeof(uint32_t) * 2) != hipSuccess ||
+        hipMemset(w->spill[0], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES) != hipSuccess ||
+        hipMemset(w->spill[1], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES) != hipSuccess ||
         hipMemset(w->gen, 0, sizeof(uint32_t) * 2) != hipSuccess ||
         hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipMemset failed"));
@@ -1719,7 +1736,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
 }
 
 void rb_world_destroy(rb_world *w) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (w) {
         (void)hipSetDevice(w->device);
         (void)hipStreamSynchronize(w->stream);
@@ -1728,7 +1745,7 @@ void rb_world_destroy(rb_world *w) {
 }
 
 int rb_set_stream(rb_world *w, void *s) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     // work queued on the old stream (a block run's check included)
@@ -1811,7 +1828,7 @@ static void fit_period(rb_world *w, const double *qpos, bool force) {
 }
 
 int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || !qpos || !qvel) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1843,7 +1860,7 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
 }
 
 int rb_get_state(rb_world *w, double *qpos, double *qvel) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || (!qpos && !qvel)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1894,7 +1911,7 @@ int rb_get_state(rb_world *w, double *qpos, double *qvel) {
 }
 
 int rb_set_xfrc(rb_world *w, const double *xf) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1918,13 +1935,13 @@ int rb_set_xfrc(rb_world *w, const double *xf) {
 }
 
 int rb_step_async(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     return enqueue_steps(w, nsteps, dt, e, mu, thr);
 }
 
 int rb_sync(rb_world *w) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -1932,7 +1949,7 @@ int rb_sync(rb_world *w) {
 }
 
 int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (w) w->sync_call = true;
     int rc = rb_step_async(w, nsteps, dt, e, mu, thr);
     if (w) w->sync_call = false;
@@ -1942,7 +1959,7 @@ int rb_step(rb_world *w, int64_t nsteps, double dt, double e, double mu, double 
 }
 
 int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     if (w->law != RB_LAW_MUJOCO) return fail(RB_EUNSUPPORTED, "sharded stepping supports the default contact law only");
     if (!(dt > 0) || !(e >= 0) || !(mu >= 0) || !(thr >= 0)) return fail(RB_EINVAL, "invalid step parameters");
@@ -1955,7 +1972,7 @@ int rb_shard_step(rb_world *w, double dt, double e, double mu, double thr) {
 }
 
 int rb_shard_exchange_done(rb_world *w) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     // insert every body not owned here into the next table (own ones went in
@@ -1970,7 +1987,7 @@ int rb_shard_exchange_done(rb_world *w) {
 }
 
 int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     if (dev_ptr) *dev_ptr = w->snap[1 - w->sp()];
     if (shard_elems) *shard_elems = 4 * w->S;
@@ -1979,7 +1996,7 @@ int rb_gpos_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *e
 }
 
 int rb_gquat_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *elem_bytes) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     if (dev_ptr) *dev_ptr = w->boxes ? w->qsnap[1 - w->sp()] : nullptr;
     if (shard_elems) *shard_elems = w->boxes ? 4 * w->S : 0;
@@ -1988,7 +2005,7 @@ int rb_gquat_buffer(rb_world *w, void **dev_ptr, int64_t *shard_elems, int32_t *
 }
 
 int rb_comm_unique_id(void *id, int32_t bytes) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(-1);
     if (!id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
     if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
     ncclUniqueId u;
@@ -1999,7 +2016,7 @@ int rb_comm_unique_id(void *id, int32_t bytes) {
 }
 
 int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || !id || bytes < (int32_t)sizeof(ncclUniqueId)) return fail(RB_EINVAL, "null world or short id");
     if (w->comm) return fail(RB_EINVAL, "communicator already initialised");
     if (!rccl().ok) return fail(RB_ENODEV, "RCCL (librccl.so) not available");
@@ -2021,7 +2038,7 @@ int rb_shard_comm_init(rb_world *w, const void *id, int32_t bytes) {
 int p2p_nhandles(const rb_world *w) { return w->boxes ? 5 : 3; }
 
 int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || !len) return fail(RB_EINVAL, "null argument");
     const int nh = p2p_nhandles(w);
     const int64_t need = nh * (int64_t)sizeof(hipIpcMemHandle_t);
@@ -2049,7 +2066,7 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
 }
 
 int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || !all) return fail(RB_EINVAL, "null argument");
     const int nh = p2p_nhandles(w);
     const int64_t blob = nh * (int64_t)sizeof(hipIpcMemHandle_t);
@@ -2101,7 +2118,7 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
 }
 
 int rb_p2p_halo(rb_world *w, int32_t enable) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     if (!w->p2p) return fail(RB_EINVAL, "rb_p2p_halo before rb_p2p_connect");
     HIPCHK(hipSetDevice(w->device));
@@ -2125,13 +2142,13 @@ int rb_p2p_halo(rb_world *w, int32_t enable) {
 }
 
 int rb_shard_run(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     return enqueue_steps(w, nsteps, dt, e, mu, thr, true);
 }
 
 int rb_record_contacts(rb_world *w, int enable) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -2150,7 +2167,7 @@ int rb_record_contacts(rb_world *w, int enable) {
 
 int rb_get_contacts(rb_world *w, int32_t *counts, int32_t *partner, int32_t *kind, double *dist, int64_t cap,
                     int64_t *total) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || !counts) return fail(RB_EINVAL, "null argument");
     if (!w->rec_count) return fail(RB_EINVAL, "contact recording was never enabled");
     HIPCHK(hipSetDevice(w->device));
@@ -2214,32 +2231,32 @@ static int kat_common(int32_t device, int32_t dtype, int64_t n, const double *in
 }
 
 int rb_kat_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(device);
     return kat_common(device, dtype, n, in, out, 24, 10, 0);
 }
 
 int rb_kat_inertia(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(device);
     return kat_common(device, dtype, n, in, out, 7, 18, 1);
 }
 
 int rb_kat_apply(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(device);
     return kat_common(device, dtype, n, in, out, 26, 6, 2);
 }
 
 int rb_kat_pair_impulse(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(device);
     return kat_common(device, dtype, n, in, out, 27, 3, 3);
 }
 
 int rb_kat_narrow(int32_t device, int32_t dtype, int64_t n, const double *in, double *out) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(device);
     return kat_common(device, dtype, n, in, out, 22, 33, 4);
 }
 
 int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     if (law != RB_LAW_MUJOCO && law != RB_LAW_BALLS) return fail(RB_EINVAL, "unknown contact law %d", law);
     if (!(tol >= 0) || !(tol < 1e6)) return fail(RB_EINVAL, "tol must be finite and >= 0");
@@ -2302,7 +2319,7 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
 extern "C" {
 
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
@@ -2318,7 +2335,7 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
 }
 
 int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     if (n_owned) *n_owned = w->n_local;
     if (bytes) *bytes = w->bytes_per_body_step;
@@ -2326,7 +2343,7 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {
 }
 
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches) {
-    ApiScope api_scope_;
+    ApiScope api_scope_(w ? w->device : -1);
     if (!w) return fail(RB_EINVAL, "null world");
     HIPCHK(hipSetDevice(w->device));
     int rc = collect_timing(w);

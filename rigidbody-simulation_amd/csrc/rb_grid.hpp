@@ -235,33 +235,67 @@ __device__ __forceinline__ Claim claim_slot(const Grid<T> &g, const Table<T> &ta
     }
     return {b, in ? 1 : 0, old, gen, RL >= 0 ? RL : grid_rl(g.super)};
 }
-// An id past a full bucket: appended (bucket, id) to the table's spill list,
-// claimed like a slot (generation-tagged count, atomicMax then atomicAdd)
+// An id past a full bucket: (bucket, id) into the table's spill lines — the
+// line of the bucket's hash, claimed like a slot (generation-tagged count,
+// atomicMax then atomicAdd), or while that line is full the next ones (up to
+// SPILL_PROBES).  The counts keep rising past a line's pairs, so a reader
+// knows to go on to the next line.
+__device__ __forceinline__ uint32_t spill_line_of(uint32_t b) {
+    uint32_t h = b * 0x9e3779b1u;
+    h ^= h >> 15;
+    return h & (uint32_t)(SPILL_LINES - 1);
+}
 template <typename T>
 __device__ __forceinline__ void spill_insert(const Table<T> &tab, int32_t *err, uint32_t b, uint32_t tagged_id,
                                           uint32_t gen) {
     if (!tab.spill) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    auto *h = reinterpret_cast<unsigned long long *>(tab.spill);
-    atomicMax(h, (unsigned long long)gen << 32);
-    const unsigned long long old = atomicAdd(h, 1ull);
-    const uint32_t k = (uint32_t)(old >> 32) == gen ? (uint32_t)old : (uint32_t)SPILL_CAP;
-    if (k >= (uint32_t)SPILL_CAP) { atomicOr(err, ERR_BUCKET_OVERFLOW); return; }
-    uint32_t *e = tab.spill + 2 + 2 * (int64_t)k;
-    wt_store(e, b);
-    wt_store(e + 1, tagged_id);
+    uint32_t ln = spill_line_of(b);
+#pragma unroll 1
+    for (int pr = 0; pr < SPILL_PROBES; ++pr, ln = (ln + 1) & (uint32_t)(SPILL_LINES - 1)) {
+        uint32_t *line = tab.spill + (int64_t)ln * SPILL_LINE_WORDS;
+        auto *h = reinterpret_cast<unsigned long long *>(line);
+        atomicMax(h, (unsigned long long)gen << 32);
+        const unsigned long long old = atomicAdd(h, 1ull);
+        const uint32_t k = (uint32_t)(old >> 32) == gen ? (uint32_t)old : (uint32_t)SPILL_PAIRS;
+        if (k < (uint32_t)SPILL_PAIRS) {
+            wt_store(line + 2 + 2 * k, b);
+            wt_store(line + 3 + 2 * k, tagged_id);
+            return;
+        }
+    }
+    atomicOr(err, ERR_BUCKET_OVERFLOW);
 }
 // f(tagged id) for each spilled id of bucket b (buckets whose header count
-// passed BUCKET_SLOTS only: the rare path, kept compact)
+// passed BUCKET_SLOTS only: the rare path): its hashed line and the ones
+// after it, SPILL_GROUP lines (one round trip) at a time, until a line read
+// had not overflowed
 template <typename T, typename F>
 __device__ __forceinline__ void spill_scan(const Table<T> &tab, uint32_t gen, uint32_t b, F f) {
     if (!tab.spill) return;
-    const uint2 h = xld(reinterpret_cast<const uint2 *>(tab.spill));
-    const int32_t n = h.y != gen ? 0 : h.x < (uint32_t)SPILL_CAP ? (int32_t)h.x : SPILL_CAP;
-    const uint2 *e = reinterpret_cast<const uint2 *>(tab.spill + 2);
+    const uint32_t l0 = spill_line_of(b);
 #pragma unroll 1
-    for (int32_t k = 0; k < n; ++k) {
-        const uint2 v = xld(e + k);
-        if (v.x == b) f(v.y);
+    for (int pr = 0; pr < SPILL_PROBES; pr += SPILL_GROUP) {
+        uint4 v[SPILL_GROUP][SPILL_LINE_WORDS / 4];
+#pragma unroll
+        for (int g = 0; g < SPILL_GROUP; ++g) {
+            const uint32_t ln = (l0 + (uint32_t)(pr + g)) & (uint32_t)(SPILL_LINES - 1);
+            const uint4 *l = reinterpret_cast<const uint4 *>(tab.spill + (int64_t)ln * SPILL_LINE_WORDS);
+#pragma unroll
+            for (int q = 0; q < SPILL_LINE_WORDS / 4; ++q) v[g][q] = xld(l + q);
+        }
+#pragma unroll
+        for (int g = 0; g < SPILL_GROUP; ++g) {
+            const uint32_t n = v[g][0].y != gen ? 0u : v[g][0].x;
+#pragma unroll
+            for (int k = 0; k < SPILL_PAIRS; ++k) {
+                // pair k: words 2 + 2k, 3 + 2k of the line
+                const uint4 &c = v[g][(2 + 2 * k) / 4];
+                const uint32_t wb = ((2 + 2 * k) & 3) == 0 ? c.x : c.z;
+                const uint32_t wi = ((2 + 2 * k) & 3) == 0 ? c.y : c.w;
+                if ((uint32_t)k < n && wb == b) f(wi);
+            }
+            if (n <= (uint32_t)SPILL_PAIRS) return;
+        }
     }
 }
 // the header's count passed the slots: bucket b has spilled ids

@@ -57,13 +57,19 @@ template <typename T> struct Table {
     uint32_t *line;            // [H / R][R x LINE_WORDS] bucket blocks: heads, then further ids
     Snap<T> *pos;              // [H][LINE_WORDS] slot snapshots (slot s at s); nullptr: not kept
     uint32_t *gen;             // this table's generation (device word)
-    uint32_t *spill;           // ids past a full bucket: header (generation << 32 | count), then
-                               // SPILL_CAP x {bucket, tagged id}; nullptr: none (an overflow is an error)
+    uint32_t *spill;           // ids past a full bucket: SPILL_LINES lines of a header (generation
+                               // << 32 | count) and SPILL_PAIRS {bucket, tagged id}, a bucket's line
+                               // by hash (rb_grid.hpp spill_insert); nullptr: none (an overflow is an error)
 };
 // A bucket holds 30 ids; a cell with more (a pile-up: C4's sliding rows
-// reach 29 by step 700) spills the rest into its table's spill list, which
-// a search reads only for a bucket whose count passed its slots.
-constexpr int SPILL_CAP = 8192;
+// reach 29 by step 700) spills the rest into its table's spill lines: the
+// line of the bucket's hash, or the next ones while it is full.  A search
+// reads a bucket's spill line(s) only when its count passed its slots.
+constexpr int SPILL_LINE_WORDS = 32;
+constexpr int SPILL_PAIRS = (SPILL_LINE_WORDS - 2) / 2;   // 15 per line
+constexpr int SPILL_LINES = 4096;                         // 512 KB per table
+constexpr int SPILL_PROBES = 64;                          // lines tried from the hashed one (<= 960 ids of a bucket)
+constexpr int SPILL_GROUP = 1;                            // lines a scan reads per round trip
 
 constexpr int MAX_PLANES = 8;
 

@@ -174,7 +174,7 @@ void tile_step_kernel(TileParams<T> p) {
     __shared__ int32_t s_ocnt[NCOL];
     __shared__ int32_t s_ostart[NCOL + 1];
     __shared__ uint16_t s_fown[TILE_FARWIN];
-    __shared__ int32_t s_misc[8];                   // 0 far in window, 1 far owned, 2-3 scan, 4 error
+    __shared__ int32_t s_misc[8];                   // 0 far in window, 1 far owned, 2-3 scan, 4 error, 5 piles
     __shared__ int32_t s_slot[9];
 
     const int tid = threadIdx.x;
@@ -204,6 +204,7 @@ void tile_step_kernel(TileParams<T> p) {
     TSTAMP(1);
 
     // ---- 2. the window's column starts, before any record ------------------
+    constexpr int WR = 6;                            // records per column staged in registers
     int cnt = 0;
     ColSrc cs{};
     int64_t src_base[4] = {0, 0, 0, 0};
@@ -221,6 +222,7 @@ void tile_step_kernel(TileParams<T> p) {
             cnt += hi - lo;
         }
         if (bad) { s_misc[4] = 1; cnt = 0; }
+        if (cnt > WR) s_misc[5] = 1;                // a pile: loaded after the first WR (below)
     }
     int W;
     const int ex = block_scan_excl(cnt, &s_misc[2], W);
@@ -275,7 +277,6 @@ void tile_step_kernel(TileParams<T> p) {
     // after); slots past the column's count load record 0 (one shared address)
     // (every lane issues them — lanes past the window's columns fetch record
     // 0 — so no branch hides their count from the wait before the arithmetic)
-    constexpr int WR = 6;
     Snap<T> rsn[WR];
     int32_t rid[WR];
     {
@@ -353,16 +354,30 @@ void tile_step_kernel(TileParams<T> p) {
             set_wpos(f, rsn[u]);
             s_id[f] = rid[u];
         }
-        for (int r = WR; r < cnt; ++r) {             // a pile's column: one at a time
-            int rr = r;
+    }
+    // piles: the records past WR of every column, spread over all lanes (one
+    // round trip for most piles); a window index's column by binary search of
+    // the starts (the last start <= it is the non-empty column holding it)
+    if (s_misc[5]) {
+        for (int i = tid; i < W; i += TILE_THREADS) {
+            int lo = 0, hi = NCOL;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_vstart[mid] <= i) lo = mid; else hi = mid;
+            }
+            int rr = i - s_vstart[lo];
+            if (rr < WR) continue;
+            const ColSrc ks = col_sources<TC>(lo % EXT - 1, lo / EXT - 1);
             int64_t g = 0;
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                if (rr >= 0 && rr < src_n[a]) g = src_base[a] + rr;
-                rr -= src_n[a];
+                if (a >= ks.n) break;
+                const int o = s_off[ks.j[a]][ks.c[a]], n = s_off[ks.j[a]][ks.c[a] + 1] - o;
+                if (rr >= 0 && rr < n) g = (int64_t)s_slot[ks.j[a]] * p.cap + o + rr;
+                rr -= n;
             }
-            set_wpos(ex + r, p.cur.pos[g]);
-            s_id[ex + r] = p.cur.id[g];
+            set_wpos(i, p.cur.pos[g]);
+            s_id[i] = p.cur.id[g];
         }
     }
 

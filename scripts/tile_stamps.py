@@ -32,9 +32,17 @@ def main():
     L.rb_diag_tile_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     sc = scenes.make(a.config)
     with W.World(sc, max_partners=32 if a.config == "c4" else 16) as w:
-        w.step(a.warm)
-        w.step(1)
-        st = w.stats()
+        for _ in range(a.warm // 50):                # (chunks: a rollback's backoff ends between them)
+            w.step(50)
+        for _ in range(20):                          # a 2-step run that committed in the tile form
+            s0 = w.stats()                           # (the stamps: its second step's)
+            w.step(2)
+            st = w.stats()
+            if st["tile_steps"] == s0["tile_steps"] + 2 and st["tile_rollbacks"] == s0["tile_rollbacks"]:
+                break
+            print("  (single step not committed in the tile form:", {k: st[k] for k in st if k.startswith("tile")}, ")")
+        else:
+            sys.exit("no committed 2-step tile run")
         nb = st["tile_slots"]
         buf = np.zeros((nb, 12), np.uint64)
         rc = L.rb_diag_tile_stamps(buf.ctypes.data_as(ctypes.c_void_p), nb)
