@@ -50,29 +50,22 @@ def main():
     read_factor = known / (cf * 1024.0)
     write_factor = known / (cw * 1024.0)
     if P == 1:
-        bench = [sys.executable, "bench.py", "--config", cfg, "--dtype", dtype, "--no-cpu-baseline",
-                 "--steps", "200", "--warmup", "20"]
+        # bench.py's default window (steps 51-450 captured, 451-850 timed:
+        # C4's pile-ups included)
+        bench = [sys.executable, "bench.py", "--config", cfg, "--dtype", dtype, "--no-cpu-baseline"]
     else:
         # P shards stepped in one process (scripts/shard_step_run.py): each
         # rank's step kernel over its own slice, tables as in a P-GPU run
         bench = [sys.executable, "scripts/shard_step_run.py", "--config", cfg, "--dtype", dtype, "--P", str(P)]
     tag = cfg if P == 1 else f"{cfg}_p{P}"
     fv, wv = run_pmc("FETCH_SIZE", bench, tag), run_pmc("WRITE_SIZE", bench, tag)
-    # the XCD-resident block kernel (rb_xblock.hip) steps K steps per launch:
-    # its figures are kept per step, under "<config>_<dtype>_xb"
-    K = int(os.environ.get("RBHIP_XB_K", "8"))
-    fx, wx = mean_for(fv, "xblock_kernel"), mean_for(wv, "xblock_kernel")
     f = mean_for(fv, "step_kernel")
     w = mean_for(wv, "step_kernel")
-    if f is None and fx is not None:
-        f, w = fx / K, wx / K
     guide = f * 1024.0 * 2.0 + w * 1024.0
     calibrated = f * 1024.0 * read_factor + w * 1024.0 * write_factor
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
     key = f"{cfg}_{dtype}" if P == 1 else f"{cfg}_{dtype}_p{P}"
-    if fx is not None:
-        key += "_xb"
     import hashlib
     lib = os.path.join(ROOT, "rigidbody-simulation_amd", "rbhip", "librbhip.so")
     data[key] = {
@@ -87,8 +80,7 @@ def main():
                       "calibrated: factors from profiles/calib_fetch.hip (8 B/lane SoA, known bytes)",
         "calibration": {"known_bytes": known, "fetch_kb": cf, "write_kb": cw,
                         "read_factor": read_factor, "write_factor": write_factor},
-        **({"kernel": "rb::xblock_kernel", "steps_per_launch": K,
-            "per": "step (per-launch counters / K)"} if fx is not None else {"kernel": "step kernel", "per": "launch"}),
+        "kernel": "step kernel", "per": "launch",
         "note": "FETCH_SIZE counts requests leaving L2, Infinity-Cache (MALL) hits included; the x2 "
                 "read correction holds for 128-B streaming requests (the state arrays), random 64-B "
                 "gathers (buckets, candidate snapshots) count once: the true figure lies between "
