@@ -24,7 +24,6 @@ def main():
     ap.add_argument("--warm", type=int, default=700)
     ap.add_argument("--config", default="c4")
     a = ap.parse_args()
-    os.environ["RBHIP_XB"] = "0"
     from rbhip import _lib, scenes
     import rbhip.world as W
     L = _lib.load(a.lib)
