@@ -39,6 +39,7 @@ def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     dtype = sys.argv[2] if len(sys.argv) > 2 else "f64"
     P = int(sys.argv[3]) if len(sys.argv) > 3 else 1      # > 1: one rank's step kernel of a P-way strong split
+    suffix = sys.argv[4] if len(sys.argv) > 4 else ""     # e.g. "_tile" (run with RBHIP_TILE=1): a key of its own
     # calibration: known-byte kernel with the state access pattern
     exe = "/tmp/calib_fetch"
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-o", exe,
@@ -57,7 +58,7 @@ def main():
         # P shards stepped in one process (scripts/shard_step_run.py): each
         # rank's step kernel over its own slice, tables as in a P-GPU run
         bench = [sys.executable, "scripts/shard_step_run.py", "--config", cfg, "--dtype", dtype, "--P", str(P)]
-    tag = cfg if P == 1 else f"{cfg}_p{P}"
+    tag = (cfg if P == 1 else f"{cfg}_p{P}") + suffix
     fv, wv = run_pmc("FETCH_SIZE", bench, tag), run_pmc("WRITE_SIZE", bench, tag)
     f = mean_for(fv, "step_kernel")
     w = mean_for(wv, "step_kernel")
@@ -65,7 +66,7 @@ def main():
     calibrated = f * 1024.0 * read_factor + w * 1024.0 * write_factor
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(path)) if os.path.exists(path) else {}
-    key = f"{cfg}_{dtype}" if P == 1 else f"{cfg}_{dtype}_p{P}"
+    key = (f"{cfg}_{dtype}" if P == 1 else f"{cfg}_{dtype}_p{P}") + suffix
     import hashlib
     lib = os.path.join(ROOT, "rigidbody-simulation_amd", "rbhip", "librbhip.so")
     data[key] = {

@@ -52,28 +52,25 @@ template <typename T> struct LazyInvI {
 };
 
 // one contact of body i through the reference's skip rules then K2
-// (FAST: divisions by m, k and |u_t| through their reciprocals, rb_device.hpp)
-template <bool FAST = true, typename T>
+template <typename T>
 __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Contact<T> &con, V3<T> x, V3<T> n,
-                                              const BodyDiv<T> &bd, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
+                                              T m, T k, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
     if (!(con.dist < T(0))) return;                 // collision.py:74 (NaN fails too)
     if (absval(con.dist) < p.thr) return;           // collision.py:79-80
     const V3<T> r = {con.pos.x - x.x, con.pos.y - x.y, con.pos.z - x.z};   // :75
     T jn;
     V3<T> jt;
-    if (impulse<FAST>(bd.k, v, w, r, n, p.e, p.mu, jn, jt)) apply<FAST>(v, w, bd.m, invI.get(), r, n, jn, jt);
+    if (impulse(k, v, w, r, n, p.e, p.mu, jn, jt)) apply(v, w, m, invI.get(), r, n, jn, jt);
 }
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 // (XFRC false: a caller whose worlds never carry one, so no branch on it)
-template <typename T, bool XFRC = true, bool FAST = true>
-__device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, const Recip<T> &rm, LazyInvI<T> &invI,
-                                            V3<T> &v, V3<T> &w) {
-    const T m = rm.b;
+template <typename T, bool XFRC = true>
+__device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T m, LazyInvI<T> &invI, V3<T> &v,
+                                            V3<T> &w) {
     V3<T> F = {m * p.g[0], m * p.g[1], m * p.g[2]};
     if (XFRC && p.xfrc) F = {p.xfrc[l] + F.x, p.xfrc[p.S + l] + F.y, p.xfrc[2 * p.S + l] + F.z};
-    const V3<T> a = div3_by<FAST>(F, rm);
-    v = {v.x + a.x * p.dt, v.y + a.y * p.dt, v.z + a.z * p.dt};
+    v = {v.x + (F.x / m) * p.dt, v.y + (F.y / m) * p.dt, v.z + (F.z / m) * p.dt};
     if (XFRC && p.xfrc) {
         const V3<T> tdt = {p.xfrc[3 * p.S + l] * p.dt, p.xfrc[4 * p.S + l] * p.dt, p.xfrc[5 * p.S + l] * p.dt};
         const V3<T> dw = np_matvec(invI.get(), tdt);
@@ -90,7 +87,7 @@ __device__ __forceinline__ void integrate_pose(V3<T> &x, Q4<T> &qn, const Q4<T> 
     qn = {q.w + (T(0.5) * res.w) * dt, q.x + (T(0.5) * res.x) * dt, q.y + (T(0.5) * res.y) * dt,
           q.z + (T(0.5) * res.z) * dt};
     const T nq = sqroot(fmadd(qn.z, qn.z, fmadd(qn.y, qn.y, fmadd(qn.x, qn.x, qn.w * qn.w))));
-    qn = div4_by(qn, recip(nq));
+    qn = {qn.w / nq, qn.x / nq, qn.y / nq, qn.z / nq};
 }
 
 }  // namespace rb

@@ -239,7 +239,7 @@ struct rb_world {
     int64_t *flags = nullptr;      // the mailbox (MailLayout, uncached); starts with flags[P]: peer q
                                    // writes slot q when its step is done
     bool halo = false;             // rb_p2p_halo: push only the bodies a peer can reach
-    int32_t *bounds = nullptr;     // halo: [2][BOUND_COPIES][BOUND_STRIDE] own cell bounds (step parity)
+    int32_t *bounds = nullptr;     // peer-to-peer: [2][BOUND_COPIES][BOUND_STRIDE] own cell bounds (step parity)
     int32_t *push_cnt = nullptr;   // halo: [P] bodies pushed to each peer this step
     int64_t *epoch = nullptr;      // steps taken since connect (advanced by the step kernel)
     void **peer_snap_dev = nullptr;       // [2][P] device array: each rank's snapshot buffers
@@ -362,7 +362,7 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.next = insert_next ? table<T>(w, 1 - sp) : Table<T>{nullptr, nullptr, nullptr, nullptr};
     p.err = w->err;
     p.epoch = w->p2p ? w->epoch : nullptr;
-    p.bounds = w->halo ? w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE : nullptr;
+    p.bounds = w->p2p ? w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE : nullptr;   // (peer-to-peer: both modes filter by them)
     p.plist = w->plist;
     p.plist_cnt = w->plist_cnt;
     if (w->vel[0]) {
@@ -518,7 +518,7 @@ Rccl &rccl() {
 }
 
 // the peer-to-peer exchange of the next snapshot and table (parity nsp)
-template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp) {
+template <typename T> P2PParams<T> make_p2p(rb_world *w, int64_t c, int nsp) {
     P2PParams<T> pp{};
     pp.ins = make_insert<T>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local);
     pp.dst = dp<Snap<T>>(w->snap[nsp], 0);
@@ -530,6 +530,8 @@ template <typename T> P2PParams<T> make_p2p(rb_world *w, int nsp) {
     pp.P = (int32_t)w->P;
     pp.S = w->S;
     pp.timeout_ticks = 500000000;      // 5 s at 100 MHz
+    pp.bounds = w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE;
+    pp.bounds_reset = w->bounds + ((c + 1) % 2) * BOUND_COPIES * BOUND_STRIDE;
     if (w->boxes) {
         pp.peer_quat = reinterpret_cast<const T *const *>(w->peer_quat_dev + (size_t)nsp * w->P);
         pp.qdst = dp<T>(w->qsnap[nsp], 0);
@@ -587,10 +589,10 @@ int shard_exchange(rb_world *w, hipStream_t s, int64_t c) {
     if (w->p2p) {
         hipError_t pe;
         if (w->dtype == RB_F64) {
-            P2PParams<double> pp = make_p2p<double>(w, nsp);
+            P2PParams<double> pp = make_p2p<double>(w, c, nsp);
             pe = launch_p2p_exchange<double>(pp, s);
         } else {
-            P2PParams<float> pp = make_p2p<float>(w, nsp);
+            P2PParams<float> pp = make_p2p<float>(w, c, nsp);
             pe = launch_p2p_exchange<float>(pp, s);
         }
         HIPCHK(pe);
@@ -2065,6 +2067,17 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
     return RB_OK;
 }
 
+// both parities of the own cell bounds empty: the next step kernel folds
+// into one, the exchange after it resets the other
+int reset_bounds(rb_world *w) {
+    if (!w->bounds) HIPCHK(hipMalloc((void **)&w->bounds, sizeof(int32_t) * 2 * BOUND_COPIES * BOUND_STRIDE));
+    std::vector<int32_t> b((size_t)2 * BOUND_COPIES * BOUND_STRIDE, 0);
+    for (int k = 0; k < 2 * BOUND_COPIES; ++k)
+        for (int d = 0; d < 3; ++d) { b[(size_t)k * BOUND_STRIDE + d] = INT32_MAX; b[(size_t)k * BOUND_STRIDE + 3 + d] = INT32_MIN; }
+    HIPCHK(hipMemcpy(w->bounds, b.data(), sizeof(int32_t) * b.size(), hipMemcpyHostToDevice));
+    return RB_OK;
+}
+
 int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     ApiScope api_scope_(w ? w->device : -1);
     if (!w || !all) return fail(RB_EINVAL, "null argument");
@@ -2111,6 +2124,8 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     HIPCHK(hipMemcpy(w->peer_flags_dev, flags.data(), sizeof(int64_t *) * flags.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(w->epoch, 0, sizeof(int64_t)));
     HIPCHK(hipMemset(w->flags, 0, sizeof(int64_t) * w->P));
+    // the own cell bounds (both modes filter the peers' bodies by them)
+    if (int rc = reset_bounds(w)) return rc;
     HIPCHK(hipDeviceSynchronize());
     w->p2p = true;
     drop_graphs(w);
@@ -2124,16 +2139,8 @@ int rb_p2p_halo(rb_world *w, int32_t enable) {
     HIPCHK(hipSetDevice(w->device));
     HIPCHK(hipStreamSynchronize(w->stream));
     if (enable) {
-        if (!w->bounds) {
-            HIPCHK(hipMalloc((void **)&w->bounds, sizeof(int32_t) * 2 * BOUND_COPIES * BOUND_STRIDE));
-            HIPCHK(hipMalloc((void **)&w->push_cnt, sizeof(int32_t) * w->P));
-        }
-        // both parities empty: the next step kernel accumulates into one, its
-        // push kernel resets the other
-        std::vector<int32_t> b((size_t)2 * BOUND_COPIES * BOUND_STRIDE, 0);
-        for (int k = 0; k < 2 * BOUND_COPIES; ++k)
-            for (int d = 0; d < 3; ++d) { b[(size_t)k * BOUND_STRIDE + d] = INT32_MAX; b[(size_t)k * BOUND_STRIDE + 3 + d] = INT32_MIN; }
-        HIPCHK(hipMemcpy(w->bounds, b.data(), sizeof(int32_t) * b.size(), hipMemcpyHostToDevice));
+        if (!w->push_cnt) HIPCHK(hipMalloc((void **)&w->push_cnt, sizeof(int32_t) * w->P));
+        if (int rc = reset_bounds(w)) return rc;
         HIPCHK(hipMemset(w->push_cnt, 0, sizeof(int32_t) * w->P));
     }
     if (w->halo != (enable != 0)) drop_graphs(w);

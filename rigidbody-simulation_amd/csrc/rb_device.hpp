@@ -137,68 +137,8 @@ template <typename T> __device__ M3<T> inertia_world(V3<T> I, Q4<T> q) {
 // once per body-step instead of once per contact (the same value)
 template <typename T> __device__ __forceinline__ T impulse_k(T m) { return (T(1) / m) + (T(1) / T(18)); }
 
-// Division by a divisor used more than once (a body's m and k, a contact's
-// |u_t|), bit-identical to a / b: with y = RN(1/b), q = RN(a y) lies within
-// an ulp of a/b, r = a - b q is exact (one fma), and RN(q + r y) = RN(a/b)
-// (Markstein's theorem) — for a, b and q away from the ends of the exponent
-// range (no overflow, underflow or sub-normal on the way); zeros, sub-normal,
-// huge, infinite and NaN operands take the IEEE division itself.  Three
-// dependent operations instead of the division's nine; checked bit for bit
-// against the division on 4 x 10^8 random pairs per precision, the fast path
-// on ~9 in 10 of them (scripts/div_check.c).
-template <typename T> __device__ __forceinline__ bool div_safe(T a) {
-    const T x = absval(a);
-    if constexpr (sizeof(T) == 8) return x >= 0x1p-900 && x <= 0x1p900;
-    else return x >= 0x1p-100f && x <= 0x1p100f;
-}
-template <typename T> struct Recip {
-    T b, y;          // divisor, RN(1 / b)
-    bool ok;         // b in the fast path's range
-};
-template <typename T> __device__ __forceinline__ Recip<T> recip(T b) { return Recip<T>{b, T(1) / b, div_safe(b)}; }
-// one quotient's fast form, and whether it is exact: a zero dividend gives
-// the signed zero a / b gives (a y: the correction step would lose the
-// sign), any other dividend needs a and q = RN(a y) in the safe range
-template <typename T> __device__ __forceinline__ T div_fast(T a, const Recip<T> &d, bool &ok) {
-    const T q = a * d.y;
-    ok = ok && (a == T(0) || (div_safe(a) && div_safe(q)));
-    return a == T(0) ? q : fmadd(fmadd(-d.b, q, a), d.y, q);
-}
-// FAST false: the IEEE division only (the cooperative form, whose register
-// budget of three waves per SIMD has no room for both paths)
-template <bool FAST = true, typename T> __device__ __forceinline__ T div_by(T a, const Recip<T> &d) {
-    if constexpr (!FAST) return a / d.b;
-    bool ok = d.ok;
-    const T q = div_fast(a, d, ok);
-    return ok ? q : a / d.b;
-}
-// three quotients by one divisor, one branch for the rare slow path
-template <bool FAST = true, typename T> __device__ __forceinline__ V3<T> div3_by(V3<T> a, const Recip<T> &d) {
-    if constexpr (!FAST) return V3<T>{a.x / d.b, a.y / d.b, a.z / d.b};
-    bool ok = d.ok;
-    V3<T> q = {div_fast(a.x, d, ok), div_fast(a.y, d, ok), div_fast(a.z, d, ok)};
-    if (!ok) q = {a.x / d.b, a.y / d.b, a.z / d.b};
-    return q;
-}
-// a quaternion's four components by one divisor (the integration's norm)
-template <bool FAST = true, typename T> __device__ __forceinline__ Q4<T> div4_by(Q4<T> a, const Recip<T> &d) {
-    if constexpr (!FAST) return Q4<T>{a.w / d.b, a.x / d.b, a.y / d.b, a.z / d.b};
-    bool ok = d.ok;
-    Q4<T> q = {div_fast(a.w, d, ok), div_fast(a.x, d, ok), div_fast(a.y, d, ok), div_fast(a.z, d, ok)};
-    if (!ok) q = {a.w / d.b, a.x / d.b, a.y / d.b, a.z / d.b};
-    return q;
-}
-// a body's divisors: m, and k = 1/m + 1/18 (impulse_k: the same value)
-template <typename T> struct BodyDiv {
-    Recip<T> m, k;
-};
-template <typename T> __device__ __forceinline__ BodyDiv<T> body_div(T m) {
-    const Recip<T> rm = recip(m);
-    return BodyDiv<T>{rm, recip(rm.y + T(1) / T(18))};
-}
-
-template <bool FAST = true, typename T>
-__device__ __forceinline__ bool impulse(const Recip<T> &k, V3<T> v, V3<T> w, V3<T> r, V3<T> n, T e, T mu,
+template <typename T>
+__device__ __forceinline__ bool impulse(T k, V3<T> v, V3<T> w, V3<T> r, V3<T> n, T e, T mu,
                                         T& jn_out, V3<T>& jt_out) {
     const V3<T> c = np_cross(w, r);
     const V3<T> u = {v.x + c.x, v.y + c.y, v.z + c.z};
@@ -206,26 +146,23 @@ __device__ __forceinline__ bool impulse(const Recip<T> &k, V3<T> v, V3<T> w, V3<
     const V3<T> ut = {u.x - un * n.x, u.y - un * n.y, u.z - un * n.z};
     jt_out = {T(0), T(0), T(0)};
     if (un >= T(0)) { jn_out = T(0); return false; }
-    const T jn = div_by<FAST>(-(T(1) + e) * un, k);
+    const T jn = (-(T(1) + e) * un) / k;
     const T nut = sqroot(np_dot(ut, ut));
     if (nut > T(1e-6)) {
         const T mf = mu * absval(jn);
         const T s = -((nut < mf) ? nut : mf);
-        const Recip<T> rn = recip(nut);
-        const V3<T> d = div3_by<FAST>(ut, rn);
-        jt_out = {s * d.x, s * d.y, s * d.z};
+        jt_out = {s * (ut.x / nut), s * (ut.y / nut), s * (ut.z / nut)};
     }
     jn_out = jn;
     return true;
 }
 
-template <bool FAST = true, typename T>
-__device__ __forceinline__ void apply(V3<T>& v, V3<T>& w, const Recip<T> &m, const M3<T>& invI, V3<T> r, V3<T> n,
+template <typename T>
+__device__ __forceinline__ void apply(V3<T>& v, V3<T>& w, T m, const M3<T>& invI, V3<T> r, V3<T> n,
                                       T jn, V3<T> jt) {
     const V3<T> P = {jn * n.x + jt.x, jn * n.y + jt.y, jn * n.z + jt.z};
     const V3<T> dw = np_matvec(invI, np_cross(r, P));
-    const V3<T> dv = div3_by<FAST>(P, m);
-    v = {v.x + dv.x, v.y + dv.y, v.z + dv.z};
+    v = {v.x + P.x / m, v.y + P.y / m, v.z + P.z / m};
     w = {w.x + dw.x, w.y + dw.y, w.z + dw.z};
 }
 
@@ -336,7 +273,9 @@ __device__ __forceinline__ bool sphere_sphere(V3<T> c1, T r1, V3<T> c2, T r2, Co
     if (cdist > (T(0) + r1) + r2) return false;
     con.dist = (cdist - r1) - r2;
     V3<T> f = {c2.x - c1.x, c2.y - c1.y, c2.z - c1.z};
-    const T len = sqroot(mj_dot(f, f));
+    // |f| is cdist bit for bit: f = -dif exactly (round-to-nearest is
+    // symmetric), so mj_dot(f, f) == mj_dot(dif, dif) — one square root less
+    const T len = cdist;
     if (len < T(1e-15)) f = {T(1), T(0), T(0)};
     else { const T inv = T(1) / len; f = {f.x * inv, f.y * inv, f.z * inv}; }
     const T s = r1 + con.dist / T(2);

@@ -206,6 +206,12 @@ template <typename T> struct P2PParams {
     // copied for the box bodies into the local one (else nullptr)
     const T *const *peer_quat;
     T *qdst;
+    // this step's own cell bounds (the step kernel's copies, reduced per
+    // block) and the other parity's copies, reset for the next step kernel:
+    // a peer's body is inserted only within a cell of them (all of them are
+    // still copied into the snapshot)
+    const int32_t *bounds;
+    int32_t *bounds_reset;
 };
 
 // Halo exchange (rb_p2p.hip), for large shards: instead of reading every

@@ -325,11 +325,11 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     const Q4<T> q = in.q;
     V3<T> v = in.v;
     V3<T> w = in.w;
-    const BodyDiv<T> bd = body_div(in.m);       // m and k = 1/m + 1/18 (impulse_k), with reciprocals
-    constexpr bool FD = PM != 1;                // (the cooperative form: IEEE divisions, rb_device.hpp)
+    const T m = in.m;
 
     // ---- a4: gravity / applied force (collision.py:66-70) ------------------
-    if (!forced) apply_force<T, true, FD>(p, l, bd.m, invI, v, w);
+    if (!forced) apply_force(p, l, m, invI, v, w);
+    const T k = impulse_k(m);
 
     STAMP(3);
     int32_t nrec = nrec_in;
@@ -342,7 +342,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
             Contact<T> con;
             if (!plane_sphere(pn, pp, x, sz.x, con)) continue;
             record(p, l, nrec, -1 - pl, 0, con.dist);
-            solve_contact<FD>(p, con, x, con.frame, bd, invI, v, w);
+            solve_contact(p, con, x, con.frame, m, k, invI, v, w);
         }
     }
     M3<T> M;                                       // box orientation (mj_kinematics of the free joint)
@@ -358,7 +358,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                 if (!plane_box_corner(pn, x, dist, M, sz, c, con)) continue;
                 ++cnt;
                 record(p, l, nrec, -1 - pl, 1 + c, con.dist);
-                solve_contact<FD>(p, con, x, con.frame, bd, invI, v, w);
+                solve_contact(p, con, x, con.frame, m, k, invI, v, w);
             }
         }
     }
@@ -430,7 +430,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                         record(p, l, nrec, j, ck, con.dist);
                         const V3<T> n = (p.oriented && self_g1) ? V3<T>{-con.frame.x, -con.frame.y, -con.frame.z}
                                                                 : con.frame;
-                        solve_contact<FD>(p, con, x, n, bd, invI, v, w);
+                        solve_contact(p, con, x, n, m, k, invI, v, w);
                     };
                     M3<T> Mj;
                     const V3<T> hj = {p.cs.sx()[j], p.cs.sy()[j], p.cs.sz()[j]};
@@ -466,7 +466,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
                 n = con.frame;
             }
             record(p, l, nrec, j, 16, con.dist);
-            solve_contact<FD>(p, con, x, n, bd, invI, v, w);
+            solve_contact(p, con, x, n, m, k, invI, v, w);
         }
     }
     if (p.rec_count) p.rec_count[l] = nrec;
@@ -497,7 +497,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     Q4<T> qn = {q.w + (T(0.5) * res.w) * p.dt, q.x + (T(0.5) * res.x) * p.dt,
                 q.y + (T(0.5) * res.y) * p.dt, q.z + (T(0.5) * res.z) * p.dt};
     const T nq = sqroot(fmadd(qn.z, qn.z, fmadd(qn.y, qn.y, fmadd(qn.x, qn.x, qn.w * qn.w))));
-    qn = div4_by<FD>(qn, recip(nq));
+    qn = {qn.w / nq, qn.x / nq, qn.y / nq, qn.z / nq};
     wt_store(p.st.vx() + l, v.x); wt_store(p.st.vy() + l, v.y); wt_store(p.st.vz() + l, v.z);
     wt_store(p.st.wx() + l, w.x); wt_store(p.st.wy() + l, w.y); wt_store(p.st.wz() + l, w.z);
     wt_store(p.st.qw() + l, qn.w); wt_store(p.st.qx() + l, qn.x); wt_store(p.st.qy() + l, qn.y);
@@ -581,7 +581,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
                                                        defer, [&] {
                 invI.get();
                 if (!p.xfrc) {
-                    apply_force(p, l, recip(in.m), invI, in.v, in.w);
+                    apply_force(p, l, in.m, invI, in.v, in.w);
                     forced = true;
                 }
             });
@@ -598,7 +598,7 @@ __device__ __forceinline__ void body_step(const StepParams<T> &p, const Lead<T> 
                                           gen, defer, [&] {
                                               invI.get();
                                               if (!p.xfrc) {
-                                                  apply_force<T, true, false>(p, l, recip(in.m), invI, in.v, in.w);
+                                                  apply_force(p, l, in.m, invI, in.v, in.w);
                                                   forced = true;
                                               }
                                           });
@@ -713,14 +713,14 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
         invI.q = in.q;
         m = invI.get();
         if (!p.xfrc) {
-            apply_force<T, true, WIDE>(p, l, recip(in.m), invI, in.v, in.w);
+            apply_force(p, l, in.m, invI, in.v, in.w);
             // a body's plane contacts come first in its contact order
             // (body_update: a sphere's one per plane, a box's corners), so
             // they are solved here too
             const int32_t kind = ld.cs.kind[i];
             const Snap<T> self = ld.snap_cur[i];
             const V3<T> x = {self.x, self.y, self.z};
-            const BodyDiv<T> bd = body_div(in.m);
+            const T k = impulse_k(in.m);
             if (kind == 0) {
                 const T rad = ld.cs.sx()[i];
                 for (int pl = 0; pl < p.n_planes; ++pl) {
@@ -729,7 +729,7 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
                     Contact<T> con;
                     if (!plane_sphere(pn, pp, x, rad, con)) continue;
                     record(p, l, nrec, -1 - pl, 0, con.dist);
-                    solve_contact<WIDE>(p, con, x, con.frame, bd, invI, in.v, in.w);
+                    solve_contact(p, con, x, con.frame, in.m, k, invI, in.v, in.w);
                 }
             } else {
                 const V3<T> sz = {ld.cs.sx()[i], ld.cs.sy()[i], ld.cs.sz()[i]};
@@ -744,7 +744,7 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
                         if (!plane_box_corner(pn, x, dist, M, sz, c, con)) continue;
                         ++cnt;
                         record(p, l, nrec, -1 - pl, 1 + c, con.dist);
-                        solve_contact<WIDE>(p, con, x, con.frame, bd, invI, in.v, in.w);
+                        solve_contact(p, con, x, con.frame, in.m, k, invI, in.v, in.w);
                     }
                 }
             }
@@ -987,8 +987,8 @@ __global__ void kat_impulse_kernel(int64_t n, const double *in, double *out) {
     const M3<T> invI = np_inv3(Iw);
     T jn;
     V3<T> jt;
-    impulse(body_div(m).k, v, w, r, nn, e, mu, jn, jt);
-    apply(v, w, recip(m), invI, r, nn, jn, jt);      // the reference always applies
+    impulse(impulse_k(m), v, w, r, nn, e, mu, jn, jt);
+    apply(v, w, m, invI, r, nn, jn, jt);      // the reference always applies
     double *o = out + 10 * c;
     o[0] = jn; o[1] = jt.x; o[2] = jt.y; o[3] = jt.z;
     o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = w.x; o[8] = w.y; o[9] = w.z;
@@ -1016,7 +1016,7 @@ __global__ void kat_apply_kernel(int64_t n, const double *in, double *out) {
     const V3<T> jt = {(T)a[14], (T)a[15], (T)a[16]};
     M3<T> Iw;
     for (int k = 0; k < 9; ++k) Iw.a[k] = (T)a[17 + k];
-    apply(v, w, recip(m), np_inv3(Iw), r, nn, jn, jt);
+    apply(v, w, m, np_inv3(Iw), r, nn, jn, jt);
     double *o = out + 6 * c;
     o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = w.x; o[4] = w.y; o[5] = w.z;
 }

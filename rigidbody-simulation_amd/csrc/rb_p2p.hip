@@ -11,8 +11,10 @@
 //      timeout that raises ERR_EXCHANGE instead of hanging; once raised, no
 //      later exchange waits);
 //   3. reads the other ranks' slices straight from their buffers (IPC
-//      mappings over xGMI) into its own buffer and inserts those bodies into
-//      the next step's table.
+//      mappings over xGMI) into its own buffer and inserts into the next
+//      step's table those within a cell of this rank's own bodies' cell
+//      bounds (the step kernel folds them, as in halo mode): the only ones
+//      an own body can reach next step.
 // The buffers alternate with the step parity, and a rank reaches step t+2's
 // exchange (which overwrites this parity) only after every peer has flagged
 // step t+1, i.e. finished reading it: no further synchronisation is needed.
@@ -77,6 +79,32 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
             __builtin_amdgcn_s_sleep(1);
         }
     }
+    // the own bodies' cell bounds after this step (the step kernel folded
+    // them into BOUND_COPIES copies): a peer body further than a cell from
+    // them is out of reach of every own body next step, so it is copied
+    // into the snapshot but not inserted (exact: cells are >= 2 x the reach)
+    __shared__ int32_t s_b[6];
+    if (tid < 64) {
+        const int32_t *c = p.bounds + (int64_t)tid * BOUND_STRIDE;
+        int32_t b[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) b[d] = c[d];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                b[d] = min(b[d], __shfl_xor(b[d], off));
+                b[3 + d] = max(b[3 + d], __shfl_xor(b[3 + d], off));
+            }
+        if (tid == 0)
+#pragma unroll
+            for (int d = 0; d < 6; ++d) s_b[d] = b[d];
+        if (blockIdx.x == 0) {
+            int32_t *r = p.bounds_reset + (int64_t)tid * BOUND_STRIDE;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) { r[d] = INT32_MAX; r[3 + d] = INT32_MIN; }
+        }
+    }
     __syncthreads();
     const int64_t id = (int64_t)blockIdx.x * 256 + tid;
     if (id >= p.ins.count || (id >= p.ins.skip_lo && id < p.ins.skip_hi)) return;
@@ -84,6 +112,13 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
     p.dst[id] = s;
     const bool box = p.ins.kind[id] != 0;
     if (box && p.qdst) copy_quat_sys(p.qdst + 4 * id, p.peer_quat[id / p.S] + 4 * id);
+    int32_t cx, cy, cz;
+    if (!cell_of(s.x, s.y, s.z, p.ins.grid.inv_cs, cx, cy, cz)) return;   // (the owner raised ERR_DOMAIN)
+    // empty bounds (min > max: no own body) insert nothing; int64: no overflow at +-1
+    if (!(s_b[0] <= s_b[3] && (int64_t)cx >= (int64_t)s_b[0] - 1 && (int64_t)cx <= (int64_t)s_b[3] + 1 &&
+          (int64_t)cy >= (int64_t)s_b[1] - 1 && (int64_t)cy <= (int64_t)s_b[4] + 1 &&
+          (int64_t)cz >= (int64_t)s_b[2] - 1 && (int64_t)cz <= (int64_t)s_b[5] + 1))
+        return;
     insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, (uint32_t)id | (box ? BOX_FLAG : 0u), *p.ins.tab.gen);
 }
 

@@ -300,13 +300,12 @@ void tile_step_kernel(TileParams<T> p) {
     // first impulse)
     const StepParams<T> &sp = p.sp;
     LazyInvI<T> invI;
-    BodyDiv<T> bd{};
+    T m = 0, kimp = 0;
     int32_t nrec = 0;
     V3<T> x{};
     auto phys_a = [&]() {
         x = {self.x, self.y, self.z};
         V3<T> I;
-        T m;
         if (p.ntypes == 1) {
             // one type (every body alike): the kernel's arguments, no memory
             // access — an LDS read here would wait for the window's LDS-DMA,
@@ -335,15 +334,15 @@ void tile_step_kernel(TileParams<T> p) {
         invI.q = q;
         invI.get();
         const int32_t id = idw & TILE_ID_MASK;
-        bd = body_div(m);
-        apply_force<T, false>(sp, id, bd.m, invI, v, w);   // (no xfrc: tile_eligible)
+        apply_force<T, false>(sp, id, m, invI, v, w);   // (no xfrc: tile_eligible)
+        kimp = impulse_k(m);
         for (int pl = 0; pl < sp.n_planes; ++pl) {
             const V3<T> pn = {sp.pn[pl][0], sp.pn[pl][1], sp.pn[pl][2]};
             const V3<T> pp = {sp.pp[pl][0], sp.pp[pl][1], sp.pp[pl][2]};
             Contact<T> con;
             if (!plane_sphere(pn, pp, x, self.r, con)) continue;
             record(sp, id, nrec, -1 - pl, 0, con.dist);
-            solve_contact(sp, con, x, con.frame, bd, invI, v, w);
+            solve_contact(sp, con, x, con.frame, m, kimp, invI, v, w);
         }
     };
     if (own_bin) phys_a();
@@ -500,7 +499,7 @@ void tile_step_kernel(TileParams<T> p) {
                 n = con.frame;
             }
             record(sp, id, nrec, j, 16, con.dist);
-            solve_contact(sp, con, x, n, bd, invI, v, w);
+            solve_contact(sp, con, x, n, m, kimp, invI, v, w);
         }
         if (sp.rec_count) sp.rec_count[id] = nrec;
         TSTAMP(6);

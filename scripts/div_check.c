@@ -1,5 +1,6 @@
-/* div_check.c — host check of the step kernels' reciprocal division
- * (rb_device.hpp div_by / div3_by): q = RN(a y) with y = RN(1/b), then
+/* div_check.c — host check of a reciprocal division tried in round 5 for
+ * the step kernels (measured slower on gfx950, not shipped):
+ * q = RN(a y) with y = RN(1/b), then
  * RN(q + (a - b q) y), taken only for a, b, q in the safe exponent range
  * (a zero dividend: q itself), must equal a / b bit for bit.  Random pairs
  * over narrow and wide exponent ranges, divisors of all-ones / all-zeros

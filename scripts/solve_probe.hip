@@ -40,8 +40,7 @@ void probe(const In *in, int np, StepParams<T> p, T *out, unsigned long long *cy
     invI.I = {b.I[0], b.I[1], b.I[2]};
     invI.q = {b.q[0], b.q[1], b.q[2], b.q[3]};
     invI.get();
-    const BodyDiv<T> bd = body_div(b.m);
-    const T r = b.r;
+    const T m = b.m, k = impulse_k(m), r = b.r;
     __shared__ T s_p[NP_MAX][4][64];
     for (int a = 0; a < np; ++a)
         for (int c = 0; c < 4; ++c) s_p[a][c][threadIdx.x] = b.pj[a][c];
@@ -55,7 +54,7 @@ void probe(const In *in, int np, StepParams<T> p, T *out, unsigned long long *cy
             Contact<T> con;
             const V3<T> cj = pos(a);
             sphere_sphere(x, r, cj, rad(a), con);
-            solve_contact(p, con, x, con.frame, bd, invI, v, w);
+            solve_contact(p, con, x, con.frame, m, k, invI, v, w);
         }
     } else if constexpr (VAR == 1) {
         Contact<T> cn;
@@ -64,7 +63,7 @@ void probe(const In *in, int np, StepParams<T> p, T *out, unsigned long long *cy
             const Contact<T> con = cn;
             const bool h = hn;
             if (a + 1 < np) hn = sphere_sphere(x, r, pos(a + 1), rad(a + 1), cn);
-            if (h) solve_contact(p, con, x, con.frame, bd, invI, v, w);
+            if (h) solve_contact(p, con, x, con.frame, m, k, invI, v, w);
         }
     } else {
         for (int a0 = 0; a0 < np; a0 += 4) {
@@ -75,7 +74,7 @@ void probe(const In *in, int np, StepParams<T> p, T *out, unsigned long long *cy
                 h[u] = a0 + u < np && sphere_sphere(x, r, pos(a0 + u < np ? a0 + u : 0), rad(a0 + u < np ? a0 + u : 0), con[u]);
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (h[u]) solve_contact(p, con[u], x, con[u].frame, bd, invI, v, w);
+                if (h[u]) solve_contact(p, con[u], x, con[u].frame, m, k, invI, v, w);
         }
     }
     unsigned long long t1;

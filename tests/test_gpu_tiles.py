@@ -131,6 +131,25 @@ def test_tile_rollback_replays_bit_exact(rb, oracle16, monkeypatch):
     assert st["tile_rollbacks"] >= 1 and st["tile_why"] & 1, st
 
 
+def test_tile_crowded_column_rolls_back_bit_exact(rb, oracle16, monkeypatch):
+    """A column past a slot's 128 lanes (scenes.crowded_cells: ~400 spheres
+    in one 4-m column) raises TILE_WHY_CAP on the first step: the run rolls
+    back and is replayed with the hashed forms — state bit-exact with the
+    oracle, the roll-back counted."""
+    from rbhip import scenes
+    sc = scenes.crowded_cells()
+    osc = oracle16.OracleScene(sc)
+    with _world(rb, monkeypatch, sc, True) as w:
+        w.step_async(20)
+        w.step_async(20)
+        w.sync()
+        gq, gv = w.get_state()
+        st = w.stats()
+    q, v = oracle16.step(osc, sc.qpos0, sc.qvel0, 40)
+    assert _same(gq, q) and _same(gv, v)
+    assert st["tile_rollbacks"] >= 1 and st["tile_why"] & (1 | 2), st
+
+
 def test_tile_form_declines_what_it_cannot_step(rb, monkeypatch):
     """Worlds outside the tile form's reach step with the hashed forms even
     with RBHIP_TILE=1: box bodies, applied forces."""
