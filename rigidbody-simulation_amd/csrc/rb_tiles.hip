@@ -63,9 +63,6 @@ namespace rb {
 static_assert((TILE_TC_MAX + 2) * (TILE_TC_MAX + 2) + 1 <= TILE_OFFW &&
               (TILE_TC_MAX + 2) * (TILE_TC_MAX + 2) <= TILE_THREADS, "column tables");
 static_assert(TILE_WMAX + TILE_FARWIN <= 65536, "window indices are 16-bit");
-// an LDS address for global_load_lds (a cast, not a lambda: a lambda in the
-// kernel body keeps clang from emitting the kernel's host stub)
-#define LDS_PTR(q) ((__attribute__((address_space(3))) void *)(q))
 
 __device__ __forceinline__ int32_t pmod(int32_t a, int32_t m) {
     const int32_t r = a % m;
@@ -308,8 +305,7 @@ void tile_step_kernel(TileParams<T> p) {
         V3<T> I;
         if (p.ntypes == 1) {
             // one type (every body alike): the kernel's arguments, no memory
-            // access — an LDS read here would wait for the window's LDS-DMA,
-            // a load for every load before it
+            // access (a load here would wait for every window load before it)
             m = p.types[0][0];
             I = {p.types[0][1], p.types[0][2], p.types[0][3]};
         } else {
