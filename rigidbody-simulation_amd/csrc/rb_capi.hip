@@ -286,11 +286,11 @@ struct rb_world {
     // failed run leaves the id-ordered state at the start of the first
     // failed run, which the host replays with the hashed-cell forms
     // (tile_finish) at the next sync point.
-    int tile_mode = 0;             // RBHIP_TILE: 0 off (default until it beats the hashed forms), 1 every eligible world, -1 auto (>= tile_min_bodies)
+    int tile_mode = -1;            // RBHIP_TILE: 0 off, 1 every eligible world, -1 auto (default: >= tile_min_bodies, off after a roll-back)
     int32_t tile_ntypes = 0;       // distinct (m, I) of the bodies when <= TILE_TYPES (else 0: no tile form)
     double tile_type_val[TILE_TYPES][4] = {};   // m ix iy iz of each type
     uint8_t *tile_type_of = nullptr;   // [N]
-    int64_t tile_min_bodies = 16385;
+    int64_t tile_min_bodies = 65537;    // (the hashed forms win up to C3's 65,536 bodies, the tile form above: DESIGN §4.1)
     int32_t tile_tc = 0, tile_ntx = 0, tile_nty = 0, tile_cap = TILE_THREADS;
     bool tile_fit_valid = false;
     int tile_valid_sp = -1;        // the bins of this parity hold the state at step c (-1: no bins)
@@ -1165,6 +1165,9 @@ int tile_finish(rb_world *w) {
     if (why & (TILE_WHY_CAP | TILE_WHY_WINDOW)) w->tile_fit_valid = false;   // the scene outgrew the fit
     w->tile_backoff = w->tile_backoff ? std::min(2 * w->tile_backoff, 64) : 1;
     w->tile_skip = w->tile_backoff;
+    // auto mode: a scene that outgrew the tile slots once (pile-ups) tends to
+    // keep doing so, and every retry costs a roll-back — step hashed from now on
+    if (w->tile_mode == -1) w->tile_mode = 0;
     const size_t first = std::min(ok, runs.size());
     w->c = first < runs.size() ? runs[first].c0 : w->c;
     const bool saved = w->sync_call;
@@ -1591,9 +1594,10 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_HELP_MAX_BODIES")) w->help_max = atoll(ev);
     if (const char *ev = getenv("RBHIP_WIDE_HELP")) w->wide_help = atoi(ev) != 0;
     // the cell-ordered tile form (rb_tiles.hip): RBHIP_TILE = 0 off, 1 every
-    // eligible world, -1 auto (eligible worlds of >= RBHIP_TILE_MIN_BODIES
-    // bodies); off by default while it measures slower than the hashed forms
-    // on C2/C3
+    // eligible world, -1 auto, the default (eligible worlds of >=
+    // RBHIP_TILE_MIN_BODIES bodies, until their first roll-back): it measures
+    // slower than the hashed forms up to 65,536 flat spheres (C3) and faster
+    // from 73,984 up
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_TILE_MIN_BODIES")) w->tile_min_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;

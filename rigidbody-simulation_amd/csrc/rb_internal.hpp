@@ -292,6 +292,7 @@ constexpr int32_t ERR_TILE = 1 << 22;
 enum : int32_t { TILE_WHY_CAP = 1, TILE_WHY_WINDOW = 2, TILE_WHY_FAR = 4, TILE_WHY_PARTNERS = 8, TILE_WHY_DOMAIN = 16 };
 constexpr int TILE_THREADS = 128;        // workgroup size; also the most bodies a slot steps
 constexpr int TILE_TC_MIN = 4, TILE_TC_MAX = 8;
+constexpr int TILE_OCC3_SLOTS = 1024;    // grids of more slots (> 4 two-wave workgroups per CU) size registers for 3 waves/SIMD
 constexpr int TILE_OFFW = 128;           // int32 words per bin's column table (>= (tc + 2)^2 + 1)
 constexpr int TILE_WMAX = 384;           // window records a workgroup holds in LDS
 constexpr int TILE_FARMAX = 1024;        // far-list capacity

@@ -141,8 +141,12 @@ __device__ __forceinline__ void tile_fail(const TileParams<T> &p, int why) {
     atomicOr(p.sp.err, ERR_TILE);
 }
 
-template <typename T, int MAXP, int TC>
-__global__ __launch_bounds__(TILE_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+// OCC: waves per SIMD the registers are sized for — 2 (fp64 192 VGPRs), or 3
+// (168, no scratch at MAXP 16) for grids of more slots than fit the GPU at
+// once at 2, where throughput, not one workgroup's chain, sets the step time
+// (4M flat spheres 600 -> 540 us; C3's 900 slots 16.2 -> 17.4 us, so not there)
+template <typename T, int MAXP, int TC, int OCC>
+__global__ __launch_bounds__(TILE_THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void tile_step_kernel(TileParams<T> p) {
     constexpr int EXT = TC + 2, NCOL = EXT * EXT, NQ = (NCOL + 1 + 3) / 4;
     // window records: [0, W) the bins', far bodies from FBASE, then one
@@ -167,7 +171,6 @@ void tile_step_kernel(TileParams<T> p) {
     __shared__ __attribute__((aligned(16))) int32_t s_id[WCAP + 1];   // id words
     __shared__ T s_fst[TILE_FARWIN][TILE_STW];      // own far bodies' state (staged by the far scan)
     __shared__ uint16_t s_pl[MAXP][TILE_THREADS];   // partners in discovery order (window index)
-    __shared__ uint16_t s_ps[MAXP][TILE_THREADS];   // sorted by body id
     __shared__ int32_t s_ocnt[NCOL];
     __shared__ int32_t s_ostart[NCOL + 1];
     __shared__ uint16_t s_fown[TILE_FARWIN];
@@ -469,20 +472,24 @@ void tile_step_kernel(TileParams<T> p) {
             tile_fail(p, TILE_WHY_PARTNERS);
             np_ = MAXP;
         }
-        // canonical order: ascending partner id (collision.py:72-88 walks
-        // MuJoCo's contact list; SURVEY §7 hard part 1)
-        for (int a = 0; a < np_; ++a) {
-            const int fa = s_pl[a][tid];
-            const int32_t ia = s_id[fa] & TILE_ID_MASK;
-            int r = 0;
-            for (int c = 0; c < np_; ++c) r += (s_id[s_pl[c][tid]] & TILE_ID_MASK) < ia;
-            s_ps[r][tid] = (uint16_t)fa;
-        }
         TSTAMP(5);
-        // K2: the partners in ascending id
+        // K2: the partners in the canonical order, ascending id (collision.py:72-88
+        // walks MuJoCo's contact list; SURVEY §7 hard part 1), each selected as
+        // the next larger id — no sorted copy in LDS, which leaves room for a
+        // sixth workgroup per CU
+        int32_t prev = -1;
         for (int a = 0; a < np_; ++a) {
-            const int f = s_ps[a][tid];
-            const int32_t j = s_id[f] & TILE_ID_MASK;
+            int f = 0;
+            int32_t j = INT32_MAX;
+            for (int c = 0; c < np_; ++c) {
+                const int fc = s_pl[c][tid];
+                const int32_t ic = s_id[fc] & TILE_ID_MASK;
+                if (ic > prev && ic < j) {
+                    j = ic;
+                    f = fc;
+                }
+            }
+            prev = j;
             const Snap<T> c = wpos(f);
             const V3<T> cj = {c.x, c.y, c.z};
             Contact<T> con;
@@ -650,15 +657,15 @@ __global__ __launch_bounds__(256) void tile_unbin_kernel(TileIO<T> p) {
 }
 
 // ---- launchers ----------------------------------------------------------------
-template <typename T, int MAXP>
+template <typename T, int MAXP, int OCC>
 hipError_t launch_tile_step_tc(const TileParams<T> &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.ntx * p.nty)), block(TILE_THREADS);
     switch (p.tc) {
-    case 4: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 4>), grid, block, 0, s, p); break;
-    case 5: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 5>), grid, block, 0, s, p); break;
-    case 6: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 6>), grid, block, 0, s, p); break;
-    case 7: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 7>), grid, block, 0, s, p); break;
-    case 8: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 8>), grid, block, 0, s, p); break;
+    case 4: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 4, OCC>), grid, block, 0, s, p); break;
+    case 5: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 5, OCC>), grid, block, 0, s, p); break;
+    case 6: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 6, OCC>), grid, block, 0, s, p); break;
+    case 7: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 7, OCC>), grid, block, 0, s, p); break;
+    case 8: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 8, OCC>), grid, block, 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -667,7 +674,9 @@ template <typename T> hipError_t launch_tile_step(const TileParams<T> &p, int ma
     if (p.tc < TILE_TC_MIN || p.tc > TILE_TC_MAX || p.ntx < 3 || p.nty < 3 || p.cap <= 0 || p.cap > TILE_THREADS ||
         p.ntypes < 1 || p.ntypes > TILE_TYPES)
         return hipErrorInvalidValue;
-    return maxp <= 16 ? launch_tile_step_tc<T, 16>(p, s) : launch_tile_step_tc<T, 32>(p, s);
+    if (maxp > 16) return launch_tile_step_tc<T, 32, 2>(p, s);
+    return (int64_t)p.ntx * p.nty > TILE_OCC3_SLOTS ? launch_tile_step_tc<T, 16, 3>(p, s)
+                                                    : launch_tile_step_tc<T, 16, 2>(p, s);
 }
 
 template <typename T> hipError_t launch_tile_build(const TileIO<T> &p, hipStream_t s) {

@@ -3,7 +3,7 @@ the GPU — bit identity of the state (uint64 words) after each chunk, the
 tile counters, and the time per step of both (HIP events around K
 graph-replayed steps on torch's stream).  Not part of the product.
 
-    python scripts/tile_check.py [--configs c3,c2,c4] [--chunks 5,20,20,100] [--time 200]
+    python scripts/tile_check.py [--configs c3,c2,c4,flat:1024:1024,incl:512:512] [--chunks 5,20,20,100] [--time 200]
 """
 import argparse
 import os
@@ -41,8 +41,13 @@ def main():
     from rbhip import scenes
     chunks = [int(c) for c in a.chunks.split(",")]
     for cfg in a.configs.split(","):
-        sc = scenes.make(cfg)
-        kw = {"max_partners": 32} if cfg == "c4" else {}
+        # "flat:NX:NY" / "incl:NX:NY": scenes.flat_spheres / incline_spheres(NX, NY)
+        if ":" in cfg:
+            kind, nx, ny = cfg.split(":")
+            sc = {"flat": scenes.flat_spheres, "incl": scenes.incline_spheres}[kind](int(nx), int(ny))
+        else:
+            sc = scenes.make(cfg)
+        kw = {"max_partners": 32} if cfg == "c4" or cfg.startswith("incl") else {}
         wt, wh = world(sc, True, dtype=a.dtype, **kw), world(sc, False, dtype=a.dtype, **kw)
         done = 0
         ok = True

@@ -1,7 +1,9 @@
 """The cell-ordered tile form (csrc/rb_tiles.hip) against the
 oracle and the hashed-cell forms, through the C-ABI.
 
-The form is opt-in (RBHIP_TILE=1 at world creation).  Bar: fp64 bit-exact
+The form is the default for eligible worlds of > 65,536 bodies
+(RBHIP_TILE=-1, auto); these tests force it (RBHIP_TILE=1 at world
+creation) or turn it off (0) on smaller scenes.  Bar: fp64 bit-exact
 (contacts and state, compared as uint64 words) — the tile form only changes
 where a body's candidates come from, not the arithmetic or the contact
 order.  Its failure paths (a full bin, window or far list; too many partners)
@@ -166,3 +168,28 @@ def test_tile_form_declines_what_it_cannot_step(rb, monkeypatch):
         w.step(3)
         st = w.stats()
         assert st["form"] != 5 and st["tile_steps"] == 0, st
+
+
+def test_tile_auto_mode_retires_after_rollback(rb, oracle16, monkeypatch):
+    """Auto mode (the default; RBHIP_TILE_MIN_BODIES lowered so the small
+    crowded scene qualifies): the first roll-back retires the tile form for
+    the world — every later run steps hashed, no second roll-back — and the
+    state stays bit-exact with the oracle."""
+    from rbhip import scenes
+    sc = scenes.crowded_cells()
+    osc = oracle16.OracleScene(sc)
+    monkeypatch.setenv("RBHIP_TILE_MIN_BODIES", "1")
+    monkeypatch.delenv("RBHIP_TILE", raising=False)
+    with rb.World(sc) as w:
+        monkeypatch.delenv("RBHIP_TILE_MIN_BODIES")
+        for _ in range(6):
+            w.step_async(10)
+        w.sync()
+        st0 = w.stats()
+        w.step(20)
+        gq, gv = w.get_state()
+        st = w.stats()
+    q, v = oracle16.step(osc, sc.qpos0, sc.qvel0, 80)
+    assert _same(gq, q) and _same(gv, v)
+    assert st0["tile_rollbacks"] == 1 and st["tile_rollbacks"] == 1, (st0, st)
+    assert st["form"] != 5 and st["tile_on"] == 0, st
