@@ -232,7 +232,14 @@ struct rb_world {
     int32_t *plist = nullptr;      // split form: [MAXP][S] sorted partner ids
     int32_t *plist_cnt = nullptr;  // split form: [S] partner counts
     int32_t *err = nullptr;
-    int32_t *err_host = nullptr;   // pinned
+    int32_t *err_host = nullptr;   // pinned, device-mapped (publish_err_kernel writes it)
+    int32_t *err_host_d = nullptr;
+    // err_host holds the error word as of all error-writing work enqueued so
+    // far: set by a graph launch (every captured graph ends in
+    // publish_err_kernel), cleared by every builder of kernel parameters that
+    // carry the error word and by every write to it.  rb_sync / rb_step then
+    // only synchronise the stream.
+    bool err_pub = false;
     ncclComm_t comm = nullptr;     // rb_shard_comm_init: the in-library exchange
     // peer-to-peer exchange (rb_p2p_connect)
     bool p2p = false;
@@ -337,6 +344,7 @@ template <typename T> Table<T> table(const rb_world *w, int sp) {
 // parameters of the step with counter value c
 template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt, double e, double mu, double thr,
                                               bool insert_next) {
+    w->err_pub = false;
     StepParams<T> p{};
     p.n_global = w->N;
     p.n_local = w->n_local;
@@ -388,6 +396,7 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
 
 template <typename T> InsertParams<T> make_insert(rb_world *w, int sp, int64_t first, int64_t count,
                                                   int64_t skip_lo, int64_t skip_hi) {
+    w->err_pub = false;
     InsertParams<T> ip{};
     ip.snap = dp<Snap<T>>(w->snap[sp], 0);
     ip.kind = w->kind;
@@ -452,10 +461,14 @@ int launch_one(rb_world *w, hipStream_t s, int64_t c, double dt, double e, doubl
 }
 
 int read_err(rb_world *w) {
-    HIPCHK(hipMemcpyAsync(w->err_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+    // the word reaches pinned host memory through publish_err_kernel: at the
+    // end of the last graph, or enqueued here when other error-writing work
+    // followed it (a separate launch costs ~9 us at a sync)
+    if (!w->err_pub) HIPCHK(launch_publish_err(w->err, w->err_host_d, w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
-    const int32_t bits = *w->err_host;
+    const int32_t bits = __atomic_load_n(w->err_host, __ATOMIC_ACQUIRE);
     if (bits) {
+        w->err_pub = false;
         HIPCHK(hipMemsetAsync(w->err, 0, sizeof(int32_t), w->stream));
         HIPCHK(hipStreamSynchronize(w->stream));
         return err_to_code(bits);
@@ -519,6 +532,7 @@ Rccl &rccl() {
 
 // the peer-to-peer exchange of the next snapshot and table (parity nsp)
 template <typename T> P2PParams<T> make_p2p(rb_world *w, int64_t c, int nsp) {
+    w->err_pub = false;
     P2PParams<T> pp{};
     pp.ins = make_insert<T>(w, nsp, 0, w->N, w->lo, w->lo + w->n_local);
     pp.dst = dp<Snap<T>>(w->snap[nsp], 0);
@@ -541,6 +555,7 @@ template <typename T> P2PParams<T> make_p2p(rb_world *w, int64_t c, int nsp) {
 
 // the halo exchange after the step kernel of step c (next snapshot and table nsp)
 template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
+    w->err_pub = false;
     HaloParams<T> hp{};
     hp.ins = make_insert<T>(w, nsp, 0, 0, 0, 0);
     hp.dst = dp<Snap<T>>(w->snap[nsp], 0);
@@ -695,6 +710,7 @@ int chunk_restore(rb_world *w) {
     HIPCHK(hipMemcpyAsync(w->state, o, st, hipMemcpyDeviceToDevice, w->stream));
     HIPCHK(hipMemcpyAsync(w->snap[w->sp()], o + st, sn, hipMemcpyDeviceToDevice, w->stream));
     if (w->boxes) HIPCHK(hipMemcpyAsync(w->qsnap[w->sp()], o + st + sn, sn, hipMemcpyDeviceToDevice, w->stream));
+    w->err_pub = false;
     HIPCHK(hipMemcpyAsync(w->err, o + st + 2 * sn, sizeof(int32_t), hipMemcpyDeviceToDevice, w->stream));
     if (w->boxes) HIPCHK(hipMemsetAsync(w->defer_cnt, 0, sizeof(int32_t) * 2, w->stream));
     w->primed = false;
@@ -796,7 +812,13 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
             hipGraph_t graph;
             hipGraphExec_t ex;
             HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
-            if (int rc = seq(w->cap_stream, c0)) { (void)hipStreamEndCapture(w->cap_stream, &graph); return rc; }
+            int rc = seq(w->cap_stream, c0);
+            const hipError_t pe = rc ? hipSuccess : launch_publish_err(w->err, w->err_host_d, w->cap_stream);
+            if (rc || pe != hipSuccess) {
+                (void)hipStreamEndCapture(w->cap_stream, &graph);
+                if (rc) return rc;
+                HIPCHK(pe);
+            }
             HIPCHK(hipStreamEndCapture(w->cap_stream, &graph));
             HIPCHK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
             (void)hipGraphDestroy(graph);
@@ -806,6 +828,7 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
     }
     it->second.used = ++w->graph_tick;
     HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
+    w->err_pub = true;                               // (the graph ends in publish_err_kernel)
     return RB_OK;
 }
 
@@ -1019,6 +1042,7 @@ int tile_alloc(rb_world *w) {
 }
 
 template <typename T> TileIO<T> make_tile_io(rb_world *w, int64_t c) {
+    w->err_pub = false;
     TileIO<T> p{};
     const int sp = (int)(c % 2);
     p.bins = tile_bins<T>(w, sp);
@@ -1037,6 +1061,7 @@ template <typename T> TileIO<T> make_tile_io(rb_world *w, int64_t c) {
 }
 
 template <typename T> TileParams<T> make_tile_step(rb_world *w, int64_t c, double dt, double e, double mu, double thr) {
+    w->err_pub = false;
     TileParams<T> p{};
     const int sp = (int)(c % 2);
     p.cur = tile_bins<T>(w, sp);
@@ -1157,6 +1182,7 @@ int tile_finish(rb_world *w) {
     w->tile_stats[2] += 1;
     w->tile_why_seen |= why;
     const int32_t clean = err & ~ERR_TILE;
+    w->err_pub = false;
     HIPCHK(hipMemcpyAsync(w->err, &clean, sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
     HIPCHK(hipMemsetAsync(w->tile_why, 0, sizeof(int32_t), w->stream));
     HIPCHK(hipStreamSynchronize(w->stream));
@@ -1717,7 +1743,10 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     }
     ALLOC(w->err, sizeof(int32_t));
 #undef ALLOC
-    if (hipHostMalloc((void **)&w->err_host, sizeof(int32_t), 0) != hipSuccess) return bail(fail(RB_ENOMEM, "hipHostMalloc failed"));
+    if (hipHostMalloc((void **)&w->err_host, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&w->err_host_d, w->err_host, 0) != hipSuccess)
+        return bail(fail(RB_ENOMEM, "hipHostMalloc failed"));
+    *w->err_host = 0;
     if (hipStreamCreateWithFlags(&w->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&w->cap_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipStreamCreate failed"));

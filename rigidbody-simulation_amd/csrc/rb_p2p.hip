@@ -337,3 +337,19 @@ template hipError_t launch_halo_exchange<double>(const HaloParams<double> &, hip
 template hipError_t launch_halo_exchange<float>(const HaloParams<float> &, hipStream_t);
 
 }  // namespace rb
+
+// ---- the error word to the host (rb_sync, rb_step) ----------------------------
+// One lane stores the device error word into pinned, device-mapped host memory
+// (a system-scope vector store), so the host reads it after the stream
+// synchronises without a device-to-host copy behind the stream's work.
+namespace rb {
+__global__ __launch_bounds__(64) void publish_err_kernel(const int32_t *err, int32_t *host) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(host, __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t launch_publish_err(const int32_t *err, int32_t *host_dev, hipStream_t s) {
+    hipLaunchKernelGGL(publish_err_kernel, dim3(1), dim3(64), 0, s, err, host_dev);
+    return hipGetLastError();
+}
+}  // namespace rb

@@ -467,6 +467,36 @@ def test_nonfinite_position_is_an_error(rb):
             w.step(1)
 
 
+def test_error_word_around_graph_runs(rb):
+    """Every captured graph ends by publishing the error word to pinned host
+    memory, so rb_sync after a graph only synchronises; an error-writing
+    launch enqueued after the graph (here an eager single step) must make
+    rb_sync publish again — and an error inside a graph run is reported by
+    the graph's own publish.  No stale bits after an error is cleared."""
+    from rbhip import scenes
+    sc = scenes.flat_spheres(8, 8, seed=0)
+    bad = sc.qpos0.copy()
+    bad[3, 2] = np.nan
+    with rb.World(sc) as w:
+        w.step(20)
+        w.sync()
+        w.set_state(bad, sc.qvel0)
+        w.step_async(1)                                  # eager, after the graph
+        with pytest.raises(rb.RbError, match="EDOM"):
+            w.sync()
+        w.set_state(sc.qpos0, sc.qvel0)
+        w.step(20)
+        w.sync()
+        w.set_state(bad, sc.qvel0)
+        with pytest.raises(rb.RbError, match="EDOM"):
+            w.step(20)                                   # raised inside the graph
+        w.set_state(sc.qpos0, sc.qvel0)
+        w.step(20)
+        w.sync()
+        w.step(1)
+        w.sync()
+
+
 def test_box_pair_across_shards_is_solved(rb):
     """Two cubes within bounding range, one per shard: the exchange carries
     their orientations (rb_gquat_buffer), so the pair is solved exactly as
