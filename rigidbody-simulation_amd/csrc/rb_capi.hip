@@ -793,8 +793,11 @@ int refit_from_device(rb_world *w) {
 // A sequence of launches covering K steps from step c0 (`seq(stream, c0)`),
 // captured once per start parity and replayed (rb_world::graphs, keyed by the
 // step count, parity, step parameters and variant).
+constexpr int GRAPH_NO_PUBLISH = 8;   // a graph variant without the trailing publish_err_kernel
+                                      // (guarded chunks: chunk_check reads the word itself)
 int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, double mu, double thr,
                  const std::function<int(hipStream_t, int64_t)> &seq) {
+    const bool publish = !(variant & GRAPH_NO_PUBLISH);
     auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
     auto it = w->graphs.find(key);
     if (it == w->graphs.end()) {
@@ -813,7 +816,7 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
             hipGraphExec_t ex;
             HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
             int rc = seq(w->cap_stream, c0);
-            const hipError_t pe = rc ? hipSuccess : launch_publish_err(w->err, w->err_host_d, w->cap_stream);
+            const hipError_t pe = rc || !publish ? hipSuccess : launch_publish_err(w->err, w->err_host_d, w->cap_stream);
             if (rc || pe != hipSuccess) {
                 (void)hipStreamEndCapture(w->cap_stream, &graph);
                 if (rc) return rc;
@@ -828,7 +831,7 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
     }
     it->second.used = ++w->graph_tick;
     HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
-    w->err_pub = true;                               // (the graph ends in publish_err_kernel)
+    w->err_pub = publish;                            // (the graph ends in publish_err_kernel)
     return RB_OK;
 }
 
@@ -1290,7 +1293,7 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         for (;;) {
             if (int rc = chunk_save(w)) return rc;
             w->box_kernel_on = !opt;
-            const int rc = replay(K, variant | (opt ? 4 : 0));
+            const int rc = replay(K, variant | (opt ? 4 : 0) | GRAPH_NO_PUBLISH);
             w->box_kernel_on = true;
             if (rc) return rc;
             int32_t err = 0;
