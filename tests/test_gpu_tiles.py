@@ -193,3 +193,34 @@ def test_tile_auto_mode_retires_after_rollback(rb, oracle16, monkeypatch):
     assert _same(gq, q) and _same(gv, v)
     assert st0["tile_rollbacks"] == 1 and st["tile_rollbacks"] == 1, (st0, st)
     assert st["form"] != 5 and st["tile_on"] == 0, st
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_auto_threshold_and_default_form_vs_oracle(rb, oracle16, monkeypatch, dtype):
+    """The default (auto) mode: 65,536 spheres (C3's size) step hashed,
+    65,792 (256 x 257) in the tile form — from rest, 150 steps bit-exact
+    with the oracle in both precisions (fp32 against the fp32 restatement),
+    then one recorded step with identical contact lists."""
+    from rbhip import scenes
+    monkeypatch.delenv("RBHIP_TILE", raising=False)
+    monkeypatch.delenv("RBHIP_TILE_MIN_BODIES", raising=False)
+    with rb.World(scenes.flat_spheres(256, 256, seed=3), dtype=dtype) as w:
+        w.step(4)
+        assert w.stats()["form"] != 5
+    sc = scenes.flat_spheres(256, 257, seed=3)
+    osc = oracle16.OracleScene(sc)
+    q, v = oracle16.step(osc, sc.qpos0, sc.qvel0, 150, dtype=dtype)
+    q1, v1, (cnt, par, kin, dis) = oracle16.step(osc, q, v, 1, dtype=dtype, record=True)
+    with rb.World(sc, dtype=dtype) as w:
+        w.step(150)
+        gq, gv = w.get_state()
+        assert _same(gq, q) and _same(gv, v)
+        w.record_contacts(True)
+        w.step(1)
+        gq, gv = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+        st = w.stats()
+    assert st["form"] == 5 and st["tile_steps"] == 151 and st["tile_rollbacks"] == 0, st
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert _same(gd, dis) and _same(gq, q1) and _same(gv, v1)
+    assert cnt.sum() > 0
