@@ -147,7 +147,8 @@ __device__ __forceinline__ void tile_fail(const TileParams<T> &p, int why) {
 // (4M flat spheres 600 -> 540 us; C3's 900 slots 16.2 -> 17.4 us, so not there)
 template <typename T, int MAXP, int TC, int OCC>
 __global__ __launch_bounds__(TILE_THREADS) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
-void tile_step_kernel(TileParams<T> p) {
+void tile_step_kernel(const int32_t *cur_off, int32_t ntx, int32_t nty, const uint32_t *gen_cur, const int32_t *err,
+                      const unsigned long long *far_hdr, TileParams<T> p) {
     constexpr int EXT = TC + 2, NCOL = EXT * EXT, NQ = (NCOL + 1 + 3) / 4;
     // window records: [0, W) the bins', far bodies from FBASE, then one
     // dummy slot (stores past a column's records)
@@ -184,19 +185,19 @@ void tile_step_kernel(TileParams<T> p) {
     // band of slots
     const int b = (int)blockIdx.x, xq = nslots / (int)N_XCD, xr = nslots % (int)N_XCD, xx = b % (int)N_XCD;
     const int slot = xx * xq + (xx < xr ? xx : xr) + b / (int)N_XCD;
-    const int sx = slot % p.ntx, sy = slot / p.ntx;
-    const uint32_t gen = *p.gen_cur;
-    const int32_t err0 = *p.sp.err;
-    const unsigned long long fh = *p.cur.far_hdr;
+    const int sx = slot % ntx, sy = slot / ntx;
+    const uint32_t gen = *gen_cur;
+    const int32_t err0 = *err;
+    const unsigned long long fh = *far_hdr;
 
     // ---- 1. the 3 x 3 bins' column tables (one round trip) -----------------
     for (int k = tid; k < 9 * NQ; k += TILE_THREADS) {
         const int j = k / NQ, qd = k - j * NQ;
-        const int bx = pmod(sx + j % 3 - 1, p.ntx), by = pmod(sy + j / 3 - 1, p.nty);
-        const int4 v = reinterpret_cast<const int4 *>(p.cur.off + (int64_t)(by * p.ntx + bx) * TILE_OFFW)[qd];
+        const int bx = pmod(sx + j % 3 - 1, ntx), by = pmod(sy + j / 3 - 1, nty);
+        const int4 v = reinterpret_cast<const int4 *>(cur_off + (int64_t)(by * ntx + bx) * TILE_OFFW)[qd];
         reinterpret_cast<int4 *>(&s_off[j][0])[qd] = v;
     }
-    if (tid < 9) s_slot[tid] = pmod(sy + tid / 3 - 1, p.nty) * p.ntx + pmod(sx + tid % 3 - 1, p.ntx);
+    if (tid < 9) s_slot[tid] = pmod(sy + tid / 3 - 1, nty) * ntx + pmod(sx + tid % 3 - 1, ntx);
     if (tid < 8) s_misc[tid] = 0;
     if (tid < NCOL) s_ocnt[tid] = 0;
     if (err0 & ERR_TILE) return;                     // the run already failed: it is replayed anyway
@@ -381,7 +382,7 @@ void tile_step_kernel(TileParams<T> p) {
     }
 
     // far bodies inside the window (the far list: rare)
-    const int Px = p.ntx * TC, Py = p.nty * TC;
+    const int Px = ntx * TC, Py = nty * TC;
     for (int i = tid; i < nfar; i += TILE_THREADS) {
         const Snap<T> sn = p.cur.far_pos[i];
         int32_t cx, cy;
@@ -657,15 +658,19 @@ __global__ __launch_bounds__(256) void tile_unbin_kernel(TileIO<T> p) {
 }
 
 // ---- launchers ----------------------------------------------------------------
+// the fields the step's first loads need, as leading scalar arguments that
+// gfx950 preloads into SGPRs (the unit is built with
+// -amdgpu-kernarg-preload-count, as the step kernels' Lead in rb_kernels.hip)
+#define TILE_LEAD(p) (p).cur.off, (p).ntx, (p).nty, (p).gen_cur, (p).sp.err, (p).cur.far_hdr
 template <typename T, int MAXP, int OCC>
 hipError_t launch_tile_step_tc(const TileParams<T> &p, hipStream_t s) {
     const dim3 grid((unsigned)(p.ntx * p.nty)), block(TILE_THREADS);
     switch (p.tc) {
-    case 4: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 4, OCC>), grid, block, 0, s, p); break;
-    case 5: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 5, OCC>), grid, block, 0, s, p); break;
-    case 6: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 6, OCC>), grid, block, 0, s, p); break;
-    case 7: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 7, OCC>), grid, block, 0, s, p); break;
-    case 8: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 8, OCC>), grid, block, 0, s, p); break;
+    case 4: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 4, OCC>), grid, block, 0, s, TILE_LEAD(p), p); break;
+    case 5: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 5, OCC>), grid, block, 0, s, TILE_LEAD(p), p); break;
+    case 6: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 6, OCC>), grid, block, 0, s, TILE_LEAD(p), p); break;
+    case 7: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 7, OCC>), grid, block, 0, s, TILE_LEAD(p), p); break;
+    case 8: hipLaunchKernelGGL((tile_step_kernel<T, MAXP, 8, OCC>), grid, block, 0, s, TILE_LEAD(p), p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
