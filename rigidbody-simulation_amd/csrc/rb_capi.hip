@@ -1018,6 +1018,12 @@ template <typename T> TileBins<T> tile_bins(const rb_world *w, int sp) {
     return t;
 }
 
+// tile_build / tile_alloc: the auto mode's bins would not fit (a scene spread
+// far, folded onto many mostly empty slots, or device memory short): the
+// world steps hashed from now on
+constexpr int TILE_DECLINED = 1;
+constexpr size_t TILE_AUTO_MAX_BYTES_PER_BODY = 2048;   // flat scenes need ~0.4 KB
+
 int tile_alloc(rb_world *w) {
     const size_t need = 2 * tile_bins_bytes(w);
     const size_t slots = (size_t)w->tile_ntx * w->tile_nty;
@@ -1025,12 +1031,26 @@ int tile_alloc(rb_world *w) {
         // the fill scratch is sized for the slots too
         return RB_OK;
     }
+    if (w->tile_mode == -1 && need > TILE_AUTO_MAX_BYTES_PER_BODY * (size_t)w->N) {
+        w->tile_mode = 0;
+        return TILE_DECLINED;
+    }
     HIPCHK(hipStreamSynchronize(w->stream));
     drop_graphs(w);                                  // captured bin pointers
     if (w->tile_mem) { HIPCHK(hipFree(w->tile_mem)); w->tile_mem = nullptr; }
     if (w->tile_fill) { HIPCHK(hipFree(w->tile_fill)); w->tile_fill = nullptr; }
-    HIPCHK(hipMalloc(&w->tile_mem, need));
-    HIPCHK(hipMalloc((void **)&w->tile_fill, slots * TILE_OFFW * 4));
+    if (hipMalloc(&w->tile_mem, need) != hipSuccess ||
+        hipMalloc((void **)&w->tile_fill, slots * TILE_OFFW * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        if (w->tile_mem) (void)hipFree(w->tile_mem);
+        w->tile_mem = nullptr;
+        w->tile_mem_bytes = 0;
+        if (w->tile_mode == -1) {
+            w->tile_mode = 0;
+            return TILE_DECLINED;
+        }
+        return fail(RB_ENOMEM, "tile bins: hipMalloc of %zu bytes failed", need);
+    }
     w->tile_mem_bytes = need;
     if (!w->tile_gen) {
         HIPCHK(hipMalloc((void **)&w->tile_gen, 2 * sizeof(uint32_t)));
@@ -1231,7 +1251,8 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         --w->tile_skip;                              // (back-off after a roll-back: this run steps hashed)
     } else if (tile) {
         w->state_version += 1;
-        return tile_run(w, nsteps, dt, e, mu, thr);
+        const int rc = tile_run(w, nsteps, dt, e, mu, thr);
+        if (rc != TILE_DECLINED) return rc;          // (declined: the hashed forms below)
     }
     if (int rc = finish_pending(w)) return rc;
     w->state_version += 1;

@@ -224,3 +224,29 @@ def test_auto_threshold_and_default_form_vs_oracle(rb, oracle16, monkeypatch, dt
     assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
     assert _same(gd, dis) and _same(gq, q1) and _same(gv, v1)
     assert cnt.sum() > 0
+
+
+def test_auto_mode_declines_a_spread_scene(rb, oracle16, monkeypatch):
+    """Auto mode on a scene spread far (65,792 spheres plus one 2 km away: the
+    tile grid folds onto its most slots, ~5 KB of bins per body) declines
+    the tile form and steps hashed — bit-exact with the oracle; forced
+    (RBHIP_TILE=1) the same scene steps in tile slots, bit-exact too."""
+    from rbhip import scenes
+    sc = scenes.flat_spheres(256, 257, seed=3)
+    q0 = sc.qpos0.copy()
+    q0[-1, 0] += 2000.0
+    sc = sc.with_(qpos0=q0)
+    q, v = oracle16.step(oracle16.OracleScene(sc), sc.qpos0, sc.qvel0, 30)
+    monkeypatch.delenv("RBHIP_TILE", raising=False)
+    with rb.World(sc) as w:
+        w.step(30)
+        gq, gv = w.get_state()
+        st = w.stats()
+    assert _same(gq, q) and _same(gv, v)
+    assert st["form"] != 5 and st["tile_steps"] == 0 and st["tile_on"] == 0, st
+    with _world(rb, monkeypatch, sc, True) as w:
+        w.step(30)
+        gq, gv = w.get_state()
+        st = w.stats()
+    assert _same(gq, q) and _same(gv, v)
+    assert st["form"] == 5 and st["tile_steps"] == 30, st
