@@ -307,13 +307,15 @@ def step_kernel_name(stats: dict) -> str:
     return _lib.FORM_NAMES.get(stats.get("form"), "?")
 
 
-def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str):
+def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str, tile: bool = False):
     """(upper, lower, source) HBM bytes per step-kernel launch from the
     committed PMC summary (profiles/pmc_traffic.json, profiles/collect_pmc.py);
     keyed by config and dtype for one GPU, with a _p<N> suffix for strong
-    shards.  (None, None, None) when that shape was never collected."""
+    shards and _tile when the tile form stepped the timed region.  (None,
+    None, None) when that shape was never collected."""
     rel = os.path.join("profiles", "pmc_traffic.json")
     key = f"{cfg}_{dtype}" if P == 1 or scaling == "weak" else f"{cfg}_{dtype}_p{P}"
+    key += "_tile" if tile else ""
     try:
         with open(os.path.join(ROOT, rel)) as f:
             e = json.load(f).get(key)
@@ -456,7 +458,7 @@ def main():
     bytes_per_launch = w.bytes_per_body_step * w.n_owned
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic, traffic_lower, traffic_src, traffic_same_build = traffic_from_profiles(args.config, args.dtype, P,
-                                                                                    args.scaling)
+                                                                                    args.scaling, st1.get("form") == 5)
 
     value = scene.n * args.steps / elapsed
     line = {

@@ -59,9 +59,12 @@ def main():
         # rank's step kernel over its own slice, tables as in a P-GPU run
         bench = [sys.executable, "scripts/shard_step_run.py", "--config", cfg, "--dtype", dtype, "--P", str(P)]
     tag = (cfg if P == 1 else f"{cfg}_p{P}") + suffix
+    # the hashed-cell keys average the hashed step kernels ("rb::step_kernel",
+    # which "rb::tile_step_kernel" does not contain), "_tile" the tile kernel
+    needle = "tile_step_kernel" if suffix == "_tile" else "rb::step_kernel"
     fv, wv = run_pmc("FETCH_SIZE", bench, tag), run_pmc("WRITE_SIZE", bench, tag)
-    f = mean_for(fv, "step_kernel")
-    w = mean_for(wv, "step_kernel")
+    f = mean_for(fv, needle)
+    w = mean_for(wv, needle)
     guide = f * 1024.0 * 2.0 + w * 1024.0
     calibrated = f * 1024.0 * read_factor + w * 1024.0 * write_factor
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")

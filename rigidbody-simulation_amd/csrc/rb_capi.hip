@@ -308,6 +308,8 @@ struct rb_world {
     int32_t *tile_why = nullptr;   // TILE_WHY_* bits raised (device)
     unsigned long long *tile_commits = nullptr;   // runs committed by the unbin kernel (device)
     int64_t *tile_host = nullptr;  // pinned: err, why, commits
+    int64_t *tile_pub_host = nullptr, *tile_pub_host_d = nullptr;   // pinned, mapped: why, commits (tile graphs' publish)
+    bool tile_pub = false;         // err_pub, and the last graph was a tile run's (tile_pub_host is current)
     unsigned long long tile_commits_seen = 0;
     struct TileRun { int64_t c0, n; double dt, e, mu, thr; };
     std::vector<TileRun> tile_pending;    // runs enqueued since the last check
@@ -793,11 +795,9 @@ int refit_from_device(rb_world *w) {
 // A sequence of launches covering K steps from step c0 (`seq(stream, c0)`),
 // captured once per start parity and replayed (rb_world::graphs, keyed by the
 // step count, parity, step parameters and variant).
-constexpr int GRAPH_NO_PUBLISH = 8;   // a graph variant without the trailing publish_err_kernel
-                                      // (guarded chunks: chunk_check reads the word itself)
 int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, double mu, double thr,
                  const std::function<int(hipStream_t, int64_t)> &seq) {
-    const bool publish = !(variant & GRAPH_NO_PUBLISH);
+    const bool tile_graph = (variant & 16) && w->tile_pub_host_d;   // (a tile run's: its words too)
     auto key = std::make_tuple(K, (int)(w->c % 2), dt, e, mu, thr, variant);
     auto it = w->graphs.find(key);
     if (it == w->graphs.end()) {
@@ -816,7 +816,10 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
             hipGraphExec_t ex;
             HIPCHK(hipStreamBeginCapture(w->cap_stream, hipStreamCaptureModeThreadLocal));
             int rc = seq(w->cap_stream, c0);
-            const hipError_t pe = rc || !publish ? hipSuccess : launch_publish_err(w->err, w->err_host_d, w->cap_stream);
+            const hipError_t pe = rc ? hipSuccess
+                                     : tile_graph ? launch_publish_err(w->err, w->err_host_d, w->cap_stream, w->tile_why,
+                                                                       w->tile_commits, w->tile_pub_host_d)
+                                                  : launch_publish_err(w->err, w->err_host_d, w->cap_stream);
             if (rc || pe != hipSuccess) {
                 (void)hipStreamEndCapture(w->cap_stream, &graph);
                 if (rc) return rc;
@@ -831,7 +834,8 @@ int graph_replay(rb_world *w, int64_t K, int variant, double dt, double e, doubl
     }
     it->second.used = ++w->graph_tick;
     HIPCHK(hipGraphLaunch(it->second.ex, w->stream));
-    w->err_pub = publish;                            // (the graph ends in publish_err_kernel)
+    w->err_pub = true;                               // (the graph ends in publish_err_kernel)
+    w->tile_pub = tile_graph;
     return RB_OK;
 }
 
@@ -1059,6 +1063,8 @@ int tile_alloc(rb_world *w) {
         HIPCHK(hipMemset(w->tile_why, 0, sizeof(int32_t)));
         HIPCHK(hipMemset(w->tile_commits, 0, sizeof(unsigned long long)));
         HIPCHK(hipHostMalloc((void **)&w->tile_host, 4 * sizeof(int64_t), 0));
+        HIPCHK(hipHostMalloc((void **)&w->tile_pub_host, 2 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void **)&w->tile_pub_host_d, w->tile_pub_host, 0));
         w->tile_commits_seen = 0;
     }
     return RB_OK;
@@ -1182,13 +1188,23 @@ int tile_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr)
 // by the hashed-cell forms — which report any real error themselves.
 int tile_finish(rb_world *w) {
     if (w->tile_pending.empty()) return RB_OK;
-    HIPCHK(hipMemcpyAsync(w->tile_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
-    HIPCHK(hipMemcpyAsync(w->tile_host + 1, w->tile_why, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
-    HIPCHK(hipMemcpyAsync(w->tile_host + 2, w->tile_commits, sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream));
-    HIPCHK(hipStreamSynchronize(w->stream));
-    const int32_t err = (int32_t)reinterpret_cast<int32_t *>(w->tile_host)[0];
-    const int32_t why = (int32_t)reinterpret_cast<int32_t *>(w->tile_host + 1)[0];
-    const unsigned long long commits = (unsigned long long)w->tile_host[2];
+    int32_t err, why;
+    unsigned long long commits;
+    if (w->err_pub && w->tile_pub) {
+        // the last tile graph published the three words (publish_err_kernel)
+        HIPCHK(hipStreamSynchronize(w->stream));
+        err = __atomic_load_n(w->err_host, __ATOMIC_ACQUIRE);
+        why = (int32_t)__atomic_load_n(w->tile_pub_host, __ATOMIC_ACQUIRE);
+        commits = (unsigned long long)__atomic_load_n(w->tile_pub_host + 1, __ATOMIC_ACQUIRE);
+    } else {
+        HIPCHK(hipMemcpyAsync(w->tile_host, w->err, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipMemcpyAsync(w->tile_host + 1, w->tile_why, sizeof(int32_t), hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipMemcpyAsync(w->tile_host + 2, w->tile_commits, sizeof(unsigned long long), hipMemcpyDeviceToHost, w->stream));
+        HIPCHK(hipStreamSynchronize(w->stream));
+        err = (int32_t)reinterpret_cast<int32_t *>(w->tile_host)[0];
+        why = (int32_t)reinterpret_cast<int32_t *>(w->tile_host + 1)[0];
+        commits = (unsigned long long)w->tile_host[2];
+    }
     const size_t ok = (size_t)(commits - w->tile_commits_seen);
     w->tile_commits_seen = commits;
     std::vector<rb_world::TileRun> runs;
@@ -1314,7 +1330,7 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         for (;;) {
             if (int rc = chunk_save(w)) return rc;
             w->box_kernel_on = !opt;
-            const int rc = replay(K, variant | (opt ? 4 : 0) | GRAPH_NO_PUBLISH);
+            const int rc = replay(K, variant | (opt ? 4 : 0));
             w->box_kernel_on = true;
             if (rc) return rc;
             int32_t err = 0;
@@ -1560,6 +1576,7 @@ void free_world(rb_world *w) {
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_host) (void)hipHostFree(w->tile_host);
+    if (w->tile_pub_host) (void)hipHostFree(w->tile_pub_host);
     if (w->defer_host) (void)hipHostFree(w->defer_host);
     if (w->io_q_h) (void)hipHostFree(w->io_q_h);
     if (w->io_v_h) (void)hipHostFree(w->io_v_h);

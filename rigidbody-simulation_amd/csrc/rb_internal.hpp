@@ -372,7 +372,9 @@ template <typename T> hipError_t launch_state_out(const StateIO<T> &p, bool want
 template <typename T> hipError_t launch_state_out_flat(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip
-hipError_t launch_publish_err(const int32_t *err, int32_t *host_dev, hipStream_t s);            // rb_p2p.hip
+hipError_t launch_publish_err(const int32_t *err, int32_t *host_dev, hipStream_t s,              // rb_p2p.hip
+                              const int32_t *why = nullptr, const unsigned long long *commits = nullptr,
+                              int64_t *host_tile_dev = nullptr);
 template <typename T> hipError_t launch_kat_impulse(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_inertia(int64_t n, const double *in, double *out, hipStream_t s);
 template <typename T> hipError_t launch_kat_apply(int64_t n, const double *in, double *out, hipStream_t s);

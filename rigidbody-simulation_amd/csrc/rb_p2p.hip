@@ -341,15 +341,25 @@ template hipError_t launch_halo_exchange<float>(const HaloParams<float> &, hipSt
 // ---- the error word to the host (rb_sync, rb_step) ----------------------------
 // One lane stores the device error word into pinned, device-mapped host memory
 // (a system-scope vector store), so the host reads it after the stream
-// synchronises without a device-to-host copy behind the stream's work.
+// synchronises without a device-to-host copy behind the stream's work; tile
+// runs' graphs also publish the tile form's reason bits and commit count.
 namespace rb {
-__global__ __launch_bounds__(64) void publish_err_kernel(const int32_t *err, int32_t *host) {
-    if (threadIdx.x == 0)
+__global__ __launch_bounds__(64) void publish_err_kernel(const int32_t *err, int32_t *host, const int32_t *why,
+                                                         const unsigned long long *commits, int64_t *host_tile) {
+    if (threadIdx.x == 0) {
         __hip_atomic_store(host, __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+        if (why) {
+            const int64_t wv = __hip_atomic_load(why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t cv = (int64_t)__hip_atomic_load(commits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(host_tile, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_tile + 1, cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
-hipError_t launch_publish_err(const int32_t *err, int32_t *host_dev, hipStream_t s) {
-    hipLaunchKernelGGL(publish_err_kernel, dim3(1), dim3(64), 0, s, err, host_dev);
+hipError_t launch_publish_err(const int32_t *err, int32_t *host_dev, hipStream_t s, const int32_t *why,
+                              const unsigned long long *commits, int64_t *host_tile_dev) {
+    hipLaunchKernelGGL(publish_err_kernel, dim3(1), dim3(64), 0, s, err, host_dev, why, commits, host_tile_dev);
     return hipGetLastError();
 }
 }  // namespace rb
