@@ -28,7 +28,8 @@ def main():
         with rbhip.World(sc) as w:
             del os.environ["RBHIP_TILE"]
             w.set_stream(torch.cuda.current_stream().cuda_stream)
-            w.step(2)                               # (steps 1-2: table / bins built, graphs warm below)
+            w.step(2)                               # (steps 1-2: table / bins built; the first
+                                                    # 50-step window below also captures its graph)
             done, out = 2, []
             while done + 50 <= a.steps:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
