@@ -250,3 +250,48 @@ def test_auto_mode_declines_a_spread_scene(rb, oracle16, monkeypatch):
         st = w.stats()
     assert _same(gq, q) and _same(gv, v)
     assert st["form"] == 5 and st["tile_steps"] == 30, st
+
+
+@pytest.mark.timeout(600)
+def test_tile_c3_2000_steps_vs_oracle(rb, oracle16, monkeypatch):
+    """The tile form forced onto configs[2] (65,536 spheres) for 2,000 steps
+    from rest, in async runs of 500 (the spheres land, bounce and settle):
+    bit-exact with the oracle, every step in tile slots."""
+    from rbhip import scenes
+    sc = scenes.make("c3")
+    with _world(rb, monkeypatch, sc, True) as w:
+        for _ in range(4):
+            w.step_async(500)
+        w.sync()
+        gq, gv = w.get_state()
+        st = w.stats()
+    q, v = oracle16.step(oracle16.OracleScene(sc), sc.qpos0, sc.qvel0, 2000)
+    assert _same(gq, q) and _same(gv, v)
+    assert st["tile_steps"] == 2000 and st["tile_rollbacks"] == 0, st
+
+
+@pytest.mark.timeout(600)
+def test_tile_default_one_million_vs_oracle(rb, oracle16, monkeypatch):
+    """1,048,576 spheres (1024 x 1024, grid spacing 0.19 < 2r: neighbours
+    collide on landing) in the default (auto) mode — the tile form with the
+    3-wave kernel (12k+ slots) — 80 steps, then one recorded step: state and
+    contact lists bit-exact with the oracle."""
+    from rbhip import scenes
+    monkeypatch.delenv("RBHIP_TILE", raising=False)
+    sc = scenes.flat_spheres(1024, 1024, seed=6, spacing=0.19)
+    osc = oracle16.OracleScene(sc)
+    q, v = oracle16.step(osc, sc.qpos0, sc.qvel0, 80)
+    q1, v1, (cnt, par, kin, dis) = oracle16.step(osc, q, v, 1, record=True)
+    with rb.World(sc) as w:
+        w.step(80)
+        gq, gv = w.get_state()
+        assert _same(gq, q) and _same(gv, v)
+        w.record_contacts(True)
+        w.step(1)
+        gq, gv = w.get_state()
+        gc, gp, gk, gd = w.contacts()
+        st = w.stats()
+    assert st["form"] == 5 and st["tile_steps"] == 81 and st["tile_slots"] > 1024, st
+    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    assert _same(gd, dis) and _same(gq, q1) and _same(gv, v1)
+    assert (kin == 16).sum() > 1000
