@@ -135,6 +135,12 @@ int fail(int code, const char *fmt, ...) {
                         hipGetErrorString(e_), __FILE__, __LINE__);                           \
     } while (0)
 
+// hipMemset / hipMemcpy without a stream run on the null stream, which the
+// worlds' non-blocking streams do not wait for: a fill of buffers that later
+// kernels on w->stream use is completed here before the call returns
+// (a late fill once zeroed contact counts a step had just recorded)
+#define NULL_STREAM_DONE() HIPCHK(hipStreamSynchronize(nullptr))
+
 int64_t next_pow2(int64_t v) {
     int64_t p = 1;
     while (p < v) p <<= 1;
@@ -662,6 +668,7 @@ int gen_guard(rb_world *w, int64_t nsteps) {
         HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
         HIPCHK(hipMemset(w->spill[k], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES));
     }
+    NULL_STREAM_DONE();
     w->gen_off = 1u - (uint32_t)w->c;   // prime() makes step c's generation 2
     w->primed = false;
     return RB_OK;
@@ -738,6 +745,7 @@ int grow_table(rb_world *w, bool &grown) {
             HIPCHK(hipMalloc(&w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * H));
         }
     }
+    NULL_STREAM_DONE();
     w->H = H;
     if ((w->group >> 24) & 1) {
         const int lx = (w->group >> 12) & 15, ly = (w->group >> 16) & 15;
@@ -1062,6 +1070,7 @@ int tile_alloc(rb_world *w) {
         HIPCHK(hipMalloc((void **)&w->tile_commits, sizeof(unsigned long long)));
         HIPCHK(hipMemset(w->tile_why, 0, sizeof(int32_t)));
         HIPCHK(hipMemset(w->tile_commits, 0, sizeof(unsigned long long)));
+        NULL_STREAM_DONE();
         HIPCHK(hipHostMalloc((void **)&w->tile_host, 4 * sizeof(int64_t), 0));
         HIPCHK(hipHostMalloc((void **)&w->tile_pub_host, 2 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer((void **)&w->tile_pub_host_d, w->tile_pub_host, 0));
@@ -1801,7 +1810,8 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         hipMemset(w->spill[0], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES) != hipSuccess ||
         hipMemset(w->spill[1], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES) != hipSuccess ||
         hipMemset(w->gen, 0, sizeof(uint32_t) * 2) != hipSuccess ||
-        hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess)
+        hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess ||
+        hipStreamSynchronize(nullptr) != hipSuccess)    // (the fills done: NULL_STREAM_DONE)
         return bail(fail(RB_ENODEV, "hipMemset failed"));
     std::vector<double> bound;
     int rc = w->dtype == RB_F64 ? upload_consts<double>(w, d, bound) : upload_consts<float>(w, d, bound);
@@ -2128,6 +2138,7 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
         const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
         HIPCHK(hipExtMallocWithFlags((void **)&w->flags, (size_t)lay.bytes, hipDeviceMallocUncached));
         HIPCHK(hipMemset(w->flags, 0, (size_t)lay.bytes));
+        NULL_STREAM_DONE();
     }
     hipIpcMemHandle_t h[5];
     HIPCHK(hipIpcGetMemHandle(&h[0], w->snap[0]));
@@ -2198,6 +2209,7 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     HIPCHK(hipMemcpy(w->peer_flags_dev, flags.data(), sizeof(int64_t *) * flags.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(w->epoch, 0, sizeof(int64_t)));
     HIPCHK(hipMemset(w->flags, 0, sizeof(int64_t) * w->P));
+    NULL_STREAM_DONE();
     // the own cell bounds (both modes filter the peers' bodies by them)
     if (int rc = reset_bounds(w)) return rc;
     HIPCHK(hipDeviceSynchronize());
@@ -2216,6 +2228,7 @@ int rb_p2p_halo(rb_world *w, int32_t enable) {
         if (!w->push_cnt) HIPCHK(hipMalloc((void **)&w->push_cnt, sizeof(int32_t) * w->P));
         if (int rc = reset_bounds(w)) return rc;
         HIPCHK(hipMemset(w->push_cnt, 0, sizeof(int32_t) * w->P));
+        NULL_STREAM_DONE();
     }
     if (w->halo != (enable != 0)) drop_graphs(w);
     w->halo = enable != 0;
@@ -2240,6 +2253,7 @@ int rb_record_contacts(rb_world *w, int enable) {
         HIPCHK(hipMalloc((void **)&w->rec_kind, sizeof(int32_t) * slots));
         HIPCHK(hipMalloc(&w->rec_dist, (size_t)w->esz * slots));
         HIPCHK(hipMemset(w->rec_count, 0, sizeof(int32_t) * w->S));
+        NULL_STREAM_DONE();
     }
     if (w->record != (enable != 0)) drop_graphs(w);
     w->record = enable != 0;
@@ -2360,6 +2374,7 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
             if (hipMalloc(&w->vel[k], bytes) != hipSuccess) return fail(RB_ENOMEM, "hipMalloc(%zu) failed", bytes);
             HIPCHK(hipMemset(w->vel[k], 0, bytes));
         }
+        NULL_STREAM_DONE();
     }
     if (w->law == RB_LAW_BALLS && law == RB_LAW_MUJOCO) {
         // the default law keeps positions in the snapshot: restore them

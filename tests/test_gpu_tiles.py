@@ -292,6 +292,12 @@ def test_tile_default_one_million_vs_oracle(rb, oracle16, monkeypatch):
         gc, gp, gk, gd = w.contacts()
         st = w.stats()
     assert st["form"] == 5 and st["tile_steps"] == 81 and st["tile_slots"] > 1024, st
-    assert np.array_equal(gc, cnt) and np.array_equal(gp, par) and np.array_equal(gk, kin)
+    bad = np.flatnonzero(gc != cnt)
+    go, oo = np.concatenate([[0], np.cumsum(gc)]), np.concatenate([[0], np.cumsum(cnt)])
+    detail = [(int(b), gp[go[b]:go[b + 1]].tolist(), gk[go[b]:go[b + 1]].tolist(),
+               par[oo[b]:oo[b + 1]].tolist(), kin[oo[b]:oo[b + 1]].tolist()) for b in bad[:4]]
+    assert not bad.size, f"contact counts differ at {bad.size} bodies (state@81 same: " \
+                         f"{_same(gq, q1) and _same(gv, v1)}): {detail}"
+    assert np.array_equal(gp, par) and np.array_equal(gk, kin), np.flatnonzero((gp != par) | (gk != kin))[:8]
     assert _same(gd, dis) and _same(gq, q1) and _same(gv, v1)
     assert (kin == 16).sum() > 1000
