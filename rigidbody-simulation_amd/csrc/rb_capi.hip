@@ -135,11 +135,17 @@ int fail(int code, const char *fmt, ...) {
                         hipGetErrorString(e_), __FILE__, __LINE__);                           \
     } while (0)
 
-// hipMemset / hipMemcpy without a stream run on the null stream, which the
-// worlds' non-blocking streams do not wait for: a fill of buffers that later
-// kernels on w->stream use is completed here before the call returns
-// (a late fill once zeroed contact counts a step had just recorded)
-#define NULL_STREAM_DONE() HIPCHK(hipStreamSynchronize(nullptr))
+// Every fill and copy of a world's buffers is enqueued on the world's own
+// stream (w->stream), so it is ordered with the world's kernels by
+// construction: a null-stream hipMemset / hipMemcpy is not ordered with a
+// non-blocking stream (one once zeroed contact counts a step had just
+// recorded), and a null-stream call also invalidates another thread's
+// graph capture on the device.  Copies from or into host memory the caller
+// frees on return end with a sync of that stream.
+#define WCHK(expr)                                                                            \
+    do {                                                                                      \
+        if (int rc_ = (expr)) return rc_;                                                     \
+    } while (0)
 
 int64_t next_pow2(int64_t v) {
     int64_t p = 1;
@@ -317,12 +323,39 @@ struct rb_world {
     int64_t *tile_pub_host = nullptr, *tile_pub_host_d = nullptr;   // pinned, mapped: why, commits (tile graphs' publish)
     bool tile_pub = false;         // err_pub, and the last graph was a tile run's (tile_pub_host is current)
     unsigned long long tile_commits_seen = 0;
-    struct TileRun { int64_t c0, n; double dt, e, mu, thr; };
+    // a run of steps whose check waits for the next sync point: a tile run,
+    // or one window of the resident form (res)
+    struct TileRun { int64_t c0, n; double dt, e, mu, thr; bool res; };
     std::vector<TileRun> tile_pending;    // runs enqueued since the last check
     int64_t tile_stats[4] = {};    // runs, steps committed, runs rolled back, bin builds
     int32_t tile_why_seen = 0;     // why bits of the runs rolled back (OR)
     int32_t tile_backoff = 0, tile_skip = 0;   // eligible runs to step hashed after a roll-back (doubling)
     bool tile_replaying = false;   // tile_finish's replay steps hashed
+
+    // the resident form (rb_resident.hip): windows of steps in
+    // one launch each, sphere worlds on one rank.  A window reads the
+    // id-ordered state and commits its end state back only if no slot failed
+    // (its check and roll-back are the tile runs': tile_pending, tile_finish)
+    int res_mode = 0;              // RBHIP_RESIDENT: 0 off (default until measured faster), 1 every eligible world, -1 auto (res_min..res_max bodies)
+    int64_t res_min_bodies = 4097, res_max_bodies = 131072;
+    bool res_fit_valid = false;
+    bool res_declined = false;     // the fit found no tiling (a slot over its capacity, or too many slots)
+    double res_L = 0, res_rl = 0, res_skin = 0, res_drift = 0;
+    double res_skin_frac = 1.0;    // skin = this x the largest contact reach (RBHIP_RES_SKIN)
+    int32_t res_ntx = 0, res_nty = 0;
+    int32_t res_window = 64;       // steps per window (halved after a skin / drift failure, grown back on success)
+    int32_t res_window_max = 64;   // RBHIP_RES_WINDOW
+    int32_t res_M = 8;             // list rebuild period (RBHIP_RES_REBUILD; 0: never within a window)
+    int64_t res_max_slots = 0;     // slots the GPU holds resident at once (with a margin)
+    void *res_mem = nullptr;       // counts, ids, publication, staging
+    size_t res_mem_bytes = 0;
+    uint32_t *res_epoch = nullptr; // [1] tag base of the next window (advanced by the commit kernel)
+    int32_t *res_abort = nullptr;  // [1]
+    uint64_t res_epoch_host = 1;   // the device word's value once the enqueued windows ran
+    int32_t res_backoff = 0, res_skip = 0;   // eligible runs to step otherwise after a roll-back (doubling)
+    int32_t res_fails = 0;         // roll-backs in a row (auto mode retires the form after RES_MAX_FAILS)
+    int64_t res_stats[4] = {};     // windows, steps committed, windows rolled back, fits
+    int32_t res_why_seen = 0;
 
     int sp() const { return (int)(c % 2); }
 };
@@ -330,6 +363,26 @@ struct rb_world {
 extern "C" {
 static void fit_period(rb_world *w, const double *qpos, bool force = false);   // (below)
 }
+
+namespace {
+// stream-ordered fills and copies of world buffers (WCHK above)
+int wfill(rb_world *w, void *dst, int value, size_t bytes) {
+    HIPCHK(hipMemsetAsync(dst, value, bytes, w->stream));
+    return RB_OK;
+}
+// from host memory the caller may free on return: waits for the copy
+int wput(rb_world *w, void *dst, const void *src, size_t bytes) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return RB_OK;
+}
+// into host memory: ordered after the world's work so far, waited for
+int wget(rb_world *w, void *dst, const void *src, size_t bytes) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipStreamSynchronize(w->stream));
+    return RB_OK;
+}
+}  // namespace
 
 namespace {
 
@@ -665,10 +718,9 @@ int gen_guard(rb_world *w, int64_t nsteps) {
                                   "the sharded world must be recreated");
     HIPCHK(hipStreamSynchronize(w->stream));
     for (int k = 0; k < 2; ++k) {
-        HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
-        HIPCHK(hipMemset(w->spill[k], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES));
+        WCHK(wfill(w, w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * w->H));
+        WCHK(wfill(w, w->spill[k], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES));
     }
-    NULL_STREAM_DONE();
     w->gen_off = 1u - (uint32_t)w->c;   // prime() makes step c's generation 2
     w->primed = false;
     return RB_OK;
@@ -738,14 +790,13 @@ int grow_table(rb_world *w, bool &grown) {
         HIPCHK(hipFree(w->ids[k]));
         w->ids[k] = nullptr;
         HIPCHK(hipMalloc((void **)&w->ids[k], sizeof(uint32_t) * LINE_WORDS * H));
-        HIPCHK(hipMemset(w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * H));
+        WCHK(wfill(w, w->ids[k], 0, sizeof(uint32_t) * LINE_WORDS * H));
         if (w->pos[k]) {
             HIPCHK(hipFree(w->pos[k]));
             w->pos[k] = nullptr;
             HIPCHK(hipMalloc(&w->pos[k], (size_t)w->esz * 4 * LINE_WORDS * H));
         }
     }
-    NULL_STREAM_DONE();
     w->H = H;
     if ((w->group >> 24) & 1) {
         const int lx = (w->group >> 12) & 15, ly = (w->group >> 16) & 15;
@@ -1034,7 +1085,23 @@ template <typename T> TileBins<T> tile_bins(const rb_world *w, int sp) {
 // far, folded onto many mostly empty slots, or device memory short): the
 // world steps hashed from now on
 constexpr int TILE_DECLINED = 1;
+constexpr int RES_MAX_FAILS = 6;   // resident roll-backs in a row after which auto mode retires the form
 constexpr size_t TILE_AUTO_MAX_BYTES_PER_BODY = 2048;   // flat scenes need ~0.4 KB
+
+// the words the pending runs' checks read (tile runs and resident windows)
+int tile_alloc_words(rb_world *w) {
+    if (w->tile_gen) return RB_OK;
+    HIPCHK(hipMalloc((void **)&w->tile_gen, 2 * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void **)&w->tile_why, sizeof(int32_t)));
+    HIPCHK(hipMalloc((void **)&w->tile_commits, sizeof(unsigned long long)));
+    WCHK(wfill(w, w->tile_why, 0, sizeof(int32_t)));
+    WCHK(wfill(w, w->tile_commits, 0, sizeof(unsigned long long)));
+    HIPCHK(hipHostMalloc((void **)&w->tile_host, 4 * sizeof(int64_t), 0));
+    HIPCHK(hipHostMalloc((void **)&w->tile_pub_host, 2 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&w->tile_pub_host_d, w->tile_pub_host, 0));
+    w->tile_commits_seen = 0;
+    return RB_OK;
+}
 
 int tile_alloc(rb_world *w) {
     const size_t need = 2 * tile_bins_bytes(w);
@@ -1064,19 +1131,7 @@ int tile_alloc(rb_world *w) {
         return fail(RB_ENOMEM, "tile bins: hipMalloc of %zu bytes failed", need);
     }
     w->tile_mem_bytes = need;
-    if (!w->tile_gen) {
-        HIPCHK(hipMalloc((void **)&w->tile_gen, 2 * sizeof(uint32_t)));
-        HIPCHK(hipMalloc((void **)&w->tile_why, sizeof(int32_t)));
-        HIPCHK(hipMalloc((void **)&w->tile_commits, sizeof(unsigned long long)));
-        HIPCHK(hipMemset(w->tile_why, 0, sizeof(int32_t)));
-        HIPCHK(hipMemset(w->tile_commits, 0, sizeof(unsigned long long)));
-        NULL_STREAM_DONE();
-        HIPCHK(hipHostMalloc((void **)&w->tile_host, 4 * sizeof(int64_t), 0));
-        HIPCHK(hipHostMalloc((void **)&w->tile_pub_host, 2 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
-        HIPCHK(hipHostGetDevicePointer((void **)&w->tile_pub_host_d, w->tile_pub_host, 0));
-        w->tile_commits_seen = 0;
-    }
-    return RB_OK;
+    return tile_alloc_words(w);
 }
 
 template <typename T> TileIO<T> make_tile_io(rb_world *w, int64_t c) {
@@ -1186,7 +1241,7 @@ int tile_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr)
     }
     w->tile_valid_sp = w->sp();
     w->primed = false;                               // the hashed forms' table is stale
-    w->tile_pending.push_back(rb_world::TileRun{c0, n, dt, e, mu, thr});
+    w->tile_pending.push_back(rb_world::TileRun{c0, n, dt, e, mu, thr, false});
     w->tile_stats[0] += 1;
     return RB_OK;
 }
@@ -1218,7 +1273,17 @@ int tile_finish(rb_world *w) {
     w->tile_commits_seen = commits;
     std::vector<rb_world::TileRun> runs;
     runs.swap(w->tile_pending);
-    for (size_t k = 0; k < ok && k < runs.size(); ++k) w->tile_stats[1] += runs[k].n;
+    bool res_ok = false;
+    for (size_t k = 0; k < ok && k < runs.size(); ++k) {
+        (runs[k].res ? w->res_stats[1] : w->tile_stats[1]) += runs[k].n;
+        res_ok |= runs[k].res;
+    }
+    if (res_ok) {
+        // committed windows: the form works on this scene (grow the window back)
+        w->res_fails = 0;
+        if (w->res_backoff > 0) w->res_backoff /= 2;
+        w->res_window = std::min(w->res_window_max, 2 * w->res_window);
+    }
     if (!(err & ERR_TILE)) {
         if (w->tile_backoff > 0) w->tile_backoff /= 2;
         return RB_OK;
@@ -1227,8 +1292,8 @@ int tile_finish(rb_world *w) {
     // every later one with the hashed-cell forms (guarded chunks: the
     // replay grows max_partners or refits the table as a synchronous
     // rb_step would)
-    w->tile_stats[2] += 1;
-    w->tile_why_seen |= why;
+    const size_t first = std::min(ok, runs.size());
+    const bool res_failed = first < runs.size() && runs[first].res;
     const int32_t clean = err & ~ERR_TILE;
     w->err_pub = false;
     HIPCHK(hipMemcpyAsync(w->err, &clean, sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
@@ -1236,13 +1301,28 @@ int tile_finish(rb_world *w) {
     HIPCHK(hipStreamSynchronize(w->stream));
     w->tile_valid_sp = -1;
     w->primed = false;
-    if (why & (TILE_WHY_CAP | TILE_WHY_WINDOW)) w->tile_fit_valid = false;   // the scene outgrew the fit
-    w->tile_backoff = w->tile_backoff ? std::min(2 * w->tile_backoff, 64) : 1;
-    w->tile_skip = w->tile_backoff;
-    // auto mode: a scene that outgrew the tile slots once (pile-ups) tends to
-    // keep doing so, and every retry costs a roll-back — step hashed from now on
-    if (w->tile_mode == -1) w->tile_mode = 0;
-    const size_t first = std::min(ok, runs.size());
+    if (res_failed) {
+        // a resident window: a body outran the skin (or its home tile) —
+        // shorter windows; a slot, list or import table overflowed — a new
+        // fit; then back off before the next try.  Auto mode retires the
+        // form after RES_MAX_FAILS roll-backs in a row.
+        w->res_stats[2] += 1;
+        w->res_why_seen |= why;
+        if (why & (RES_WHY_SKIN | RES_WHY_DRIFT)) w->res_window = std::max(4, w->res_window / 2);
+        if (why & (TILE_WHY_CAP | RES_WHY_LIST | RES_WHY_IMPORT)) w->res_fit_valid = false;
+        w->res_backoff = w->res_backoff ? std::min(2 * w->res_backoff, 64) : 1;
+        w->res_skip = w->res_backoff;
+        if (++w->res_fails >= RES_MAX_FAILS && w->res_mode == -1) w->res_mode = 0;
+    } else {
+        w->tile_stats[2] += 1;
+        w->tile_why_seen |= why;
+        if (why & (TILE_WHY_CAP | TILE_WHY_WINDOW)) w->tile_fit_valid = false;   // the scene outgrew the fit
+        w->tile_backoff = w->tile_backoff ? std::min(2 * w->tile_backoff, 64) : 1;
+        w->tile_skip = w->tile_backoff;
+        // auto mode: a scene that outgrew the tile slots once (pile-ups) tends to
+        // keep doing so, and every retry costs a roll-back — step hashed from now on
+        if (w->tile_mode == -1) w->tile_mode = 0;
+    }
     w->c = first < runs.size() ? runs[first].c0 : w->c;
     const bool saved = w->sync_call;
     w->sync_call = true;
@@ -1257,6 +1337,264 @@ int tile_finish(rb_world *w) {
     return rc;
 }
 
+// ---- the resident form (rb_resident.hip) ------------------------
+bool res_eligible(const rb_world *w) {
+    if (w->res_mode == 0 || w->res_declined || w->tile_replaying || w->P != 1 || !w->all_spheres ||
+        w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
+        return false;
+    if (w->maxp > 32 || w->n_local <= 0 || w->N >= (int64_t)1 << 30) return false;
+    return w->res_mode == 1 || (w->n_local >= w->res_min_bodies && w->n_local <= w->res_max_bodies);
+}
+
+// slots of one world's grid the GPU holds resident at once, with a margin
+// (workgroups are dealt round-robin over the XCDs, empty slots included)
+int64_t res_capacity(rb_world *w) {
+    if (w->res_max_slots > 0) return w->res_max_slots;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, w->device) != hipSuccess) cus = 0;
+    const int per_cu = res_blocks_per_cu(w->dtype == RB_F64, w->maxp);
+    w->res_max_slots = (int64_t)cus * per_cu * 7 / 8;
+    return w->res_max_slots;
+}
+
+// The tiling from body positions (x, y at pos[k * stride], pos[k * stride + 1]):
+// skin = res_skin_frac x the largest contact reach, list radius rl = reach +
+// 2 skin; the largest tile side L >= 1.5 rl (a drift room of rl / 4 per side
+// for windows that rebuild their lists) whose fullest tile holds at most 7/8
+// of a slot; ntx x nty slots over the scene's extent plus one ring.  A scene
+// no tiling fits (a tile over capacity at the smallest side, or more slots
+// than the GPU holds resident) is declined until its next rb_set_state.
+void res_fit(rb_world *w, const double *pos, int64_t stride) {
+    w->res_stats[3] += 1;
+    w->res_fit_valid = true;
+    w->res_declined = false;
+    const double reach = 2.0 * w->rmax;
+    w->res_skin = w->res_skin_frac * reach;
+    w->res_rl = reach + 2.0 * w->res_skin;
+    std::vector<double> xs, ys;
+    xs.reserve((size_t)w->N);
+    ys.reserve((size_t)w->N);
+    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
+    for (int64_t b = 0; b < w->N; ++b) {
+        const double x = pos[b * stride], y = pos[b * stride + 1];
+        if (!(fabs(x) < 1e9 && fabs(y) < 1e9)) continue;
+        xs.push_back(x);
+        ys.push_back(y);
+        lo[0] = std::min(lo[0], x); hi[0] = std::max(hi[0], x);
+        lo[1] = std::min(lo[1], y); hi[1] = std::max(hi[1], y);
+    }
+    if (xs.empty()) { w->res_declined = true; return; }
+    const int64_t limit = 7 * RES_CAP / 8;
+    std::vector<int64_t> t(xs.size());
+    auto worst = [&](double L) {
+        const double inv = 1.0 / L;
+        for (size_t k = 0; k < xs.size(); ++k)
+            t[k] = (((int64_t)floor(xs[k] * inv) + (1 << 30)) << 31) | ((int64_t)floor(ys[k] * inv) + (1 << 30));
+        std::sort(t.begin(), t.end());
+        int64_t m = 0;
+        for (size_t a = 0; a < t.size();) {
+            size_t e = a;
+            while (e < t.size() && t[e] == t[a]) ++e;
+            m = std::max<int64_t>(m, (int64_t)(e - a));
+            a = e;
+        }
+        return m;
+    };
+    const double Lmin = w->res_rl * 1.5;
+    if (worst(Lmin) > limit) { w->res_declined = true; return; }
+    double L = Lmin;
+    while (L < 1e6 && worst(L * 1.25) <= limit) L *= 1.25;
+    for (int k = 0; k < 6; ++k) {                    // (bisect the last factor)
+        const double mid = L * (1.0 + 0.25 / (2 << k));
+        if (worst(mid) <= limit) L = mid;
+    }
+    const int64_t ntx = (int64_t)floor(hi[0] / L) - (int64_t)floor(lo[0] / L) + 3;
+    const int64_t nty = (int64_t)floor(hi[1] / L) - (int64_t)floor(lo[1] / L) + 3;
+    if (ntx * nty > res_capacity(w) || ntx * nty > INT32_MAX / (8 * RES_CAP)) { w->res_declined = true; return; }
+    w->res_L = L;
+    w->res_ntx = (int32_t)std::max<int64_t>(3, ntx);
+    w->res_nty = (int32_t)std::max<int64_t>(3, nty);
+    w->res_drift = 0.5 * (L - w->res_rl) * (1.0 - 1e-6);
+}
+
+size_t res_bytes(const rb_world *w, size_t *o_ids, size_t *o_pub, size_t *o_snap, size_t *o_st) {
+    const size_t slots = (size_t)w->res_ntx * w->res_nty, esz = (size_t)w->esz, G = w->dtype == RB_F64 ? 6 : 3;
+    auto up = [](size_t v) { return (v + 255) / 256 * 256; };
+    size_t o = up(slots * 4);
+    *o_ids = o;
+    o += up(slots * RES_CAP * 4);
+    *o_pub = o;
+    o += up(2 * slots * G * RES_CAP * 8);
+    *o_snap = o;
+    o += up((size_t)w->Npad * 4 * esz);
+    *o_st = o;
+    o += up((size_t)10 * w->S * esz);
+    return o;
+}
+
+int res_alloc(rb_world *w) {
+    size_t oi, op, os, ot;
+    const size_t need = res_bytes(w, &oi, &op, &os, &ot);
+    if (w->res_mem && w->res_mem_bytes >= need) return RB_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);                                  // captured buffer pointers
+    if (w->res_mem) { HIPCHK(hipFree(w->res_mem)); w->res_mem = nullptr; w->res_mem_bytes = 0; }
+    if (hipMalloc(&w->res_mem, need) != hipSuccess) {
+        (void)hipGetLastError();
+        w->res_mem = nullptr;
+        if (w->res_mode == -1) { w->res_mode = 0; return TILE_DECLINED; }
+        return fail(RB_ENOMEM, "resident form: hipMalloc of %zu bytes failed", need);
+    }
+    w->res_mem_bytes = need;
+    // granule tags 0: older than every window's (res_epoch starts at 1)
+    HIPCHK(hipMemsetAsync(w->res_mem, 0, need, w->stream));
+    if (!w->res_epoch) {
+        HIPCHK(hipMalloc((void **)&w->res_epoch, 256));
+        w->res_abort = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(w->res_epoch) + 128);
+    }
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w->res_epoch, 1, 1, w->stream));
+    HIPCHK(hipMemsetAsync(w->res_abort, 0, sizeof(int32_t), w->stream));
+    w->res_epoch_host = 1;
+    if (int rc = tile_alloc_words(w)) return rc;
+    return RB_OK;
+}
+
+template <typename T> ResParams<T> make_res(rb_world *w, int64_t c0, int32_t K, bool rec, double dt, double e, double mu,
+                                            double thr) {
+    size_t oi, op, os, ot;
+    res_bytes(w, &oi, &op, &os, &ot);
+    char *m = static_cast<char *>(w->res_mem);
+    ResParams<T> p{};
+    p.sp = make_step<T>(w, c0, dt, e, mu, thr, false);   // (err_pub cleared)
+    if (!rec) {
+        p.sp.rec_count = nullptr;
+        p.sp.rec_partner = nullptr;
+        p.sp.rec_kind = nullptr;
+        p.sp.rec_dist = nullptr;
+    }
+    p.cnt = reinterpret_cast<const int32_t *>(m);
+    p.ids = reinterpret_cast<const int32_t *>(m + oi);
+    p.snap = dp<Snap<T>>(w->snap[c0 % 2], 0);
+    p.pub = reinterpret_cast<unsigned long long *>(m + op);
+    p.out_snap = reinterpret_cast<Snap<T> *>(m + os);
+    p.out_st = reinterpret_cast<T *>(m + ot);
+    p.epoch = w->res_epoch;
+    p.abort = w->res_abort;
+    p.why = w->tile_why;
+    p.ntx = w->res_ntx;
+    p.nty = w->res_nty;
+    p.K = K;
+    p.M = w->res_M > 0 && w->res_M < K ? w->res_M : 0;
+    p.L = (T)w->res_L;
+    p.inv_L = (T)(1.0 / w->res_L);
+    p.rl = (T)w->res_rl;
+    const double sk = w->res_skin * (1.0 - 1e-6);
+    p.skin2 = (T)(sk * sk);
+    p.drift = (T)w->res_drift;
+    p.rec = rec ? 1 : 0;
+    p.timeout = 5000000;                             // 50 ms of s_memrealtime (100 MHz)
+    return p;
+}
+
+template <typename T> ResCommit<T> make_res_commit(rb_world *w, int64_t c_end, int32_t K) {
+    size_t oi, op, os, ot;
+    res_bytes(w, &oi, &op, &os, &ot);
+    char *m = static_cast<char *>(w->res_mem);
+    ResCommit<T> p{};
+    p.err = w->err;
+    p.out_snap = reinterpret_cast<const Snap<T> *>(m + os);
+    p.out_st = reinterpret_cast<const T *>(m + ot);
+    p.snap = dp<Snap<T>>(w->snap[c_end % 2], 0);
+    p.st = BodyState<T>{dp<T>(w->state, 0), w->S};
+    p.n = w->N;
+    p.S = w->S;
+    p.epoch = w->res_epoch;
+    p.K = K;
+    p.abort = w->res_abort;
+    p.commits = w->tile_commits;
+    return p;
+}
+
+// One run of n steps in windows of res_window steps from step c, graph-
+// replayed (per window: clear the slot counts, bin, the resident kernel, the
+// commit), each window recorded as pending until checked.
+int res_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
+    if (!w->res_fit_valid) {
+        if (int rc = finish_pending(w)) return rc;   // (the fit reads the id-ordered state)
+        if (w->io_q_h && w->mirror_version == w->state_version) {
+            res_fit(w, w->io_q_h, 7);
+        } else {
+            std::vector<double> q((size_t)4 * w->N);
+            if (w->dtype == RB_F64) {
+                HIPCHK(hipMemcpyAsync(q.data(), w->snap[w->sp()], sizeof(double) * q.size(), hipMemcpyDeviceToHost, w->stream));
+                HIPCHK(hipStreamSynchronize(w->stream));
+            } else {
+                std::vector<float> f(q.size());
+                HIPCHK(hipMemcpyAsync(f.data(), w->snap[w->sp()], sizeof(float) * f.size(), hipMemcpyDeviceToHost, w->stream));
+                HIPCHK(hipStreamSynchronize(w->stream));
+                for (size_t k = 0; k < f.size(); ++k) q[k] = f[k];
+            }
+            res_fit(w, q.data(), 4);
+        }
+        drop_graphs(w);                              // the tiling is a captured kernel argument
+        if (w->res_declined) return TILE_DECLINED;
+    }
+    if (int rc = res_alloc(w)) return rc;
+    const bool f64 = w->dtype == RB_F64;
+    const int32_t Kw = std::max(2, w->res_window);
+    // tags are 32-bit: restart them (granules zeroed) well before they wrap
+    if (w->res_epoch_host + (uint64_t)n + (uint64_t)(n / Kw + 2) * 2 > 0xf0000000ull) {
+        HIPCHK(hipStreamSynchronize(w->stream));
+        size_t oi, op, os, ot;
+        res_bytes(w, &oi, &op, &os, &ot);
+        HIPCHK(hipMemsetAsync(static_cast<char *>(w->res_mem) + op, 0, os - op, w->stream));
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w->res_epoch, 1, 1, w->stream));
+        w->res_epoch_host = 1;
+    }
+    const size_t slots = (size_t)w->res_ntx * w->res_nty;
+    // graphs of at most 16 windows (a long run replays several)
+    const int64_t chunk = 16 * (int64_t)Kw;
+    if (n > chunk) {
+        for (int64_t left = n; left > 0;) {
+            const int64_t nn = std::min(left, chunk);
+            const bool saved = w->record;
+            w->record = saved && nn == left;         // (only the run's last step is recorded)
+            const int rc = res_run(w, nn, dt, e, mu, thr);
+            w->record = saved;
+            if (rc) return rc;
+            left -= nn;
+        }
+        return RB_OK;
+    }
+    const int64_t c0 = w->c;
+    const int variant = 16 | 64 | (int)w->record | (Kw << 8) | (w->res_M << 20);
+    int rc = graph_replay(w, n, variant, dt, e, mu, thr, [&](hipStream_t s, int64_t cs) {
+        for (int64_t k0 = 0; k0 < n; k0 += Kw) {
+            const int32_t K = (int32_t)std::min<int64_t>(Kw, n - k0);
+            const bool rec = w->record && k0 + K == n;
+            HIPCHK(hipMemsetAsync(w->res_mem, 0, slots * 4, s));
+            HIPCHK(f64 ? launch_res_bin<double>(make_res<double>(w, cs + k0, K, rec, dt, e, mu, thr), w->N, s)
+                       : launch_res_bin<float>(make_res<float>(w, cs + k0, K, rec, dt, e, mu, thr), w->N, s));
+            HIPCHK(f64 ? launch_res_step<double>(make_res<double>(w, cs + k0, K, rec, dt, e, mu, thr), w->maxp, s)
+                       : launch_res_step<float>(make_res<float>(w, cs + k0, K, rec, dt, e, mu, thr), w->maxp, s));
+            HIPCHK(f64 ? launch_res_commit<double>(make_res_commit<double>(w, cs + k0 + K, K), s)
+                       : launch_res_commit<float>(make_res_commit<float>(w, cs + k0 + K, K), s));
+        }
+        return (int)RB_OK;
+    });
+    if (rc) return rc;
+    for (int64_t k0 = 0; k0 < n; k0 += Kw) {
+        const int64_t K = std::min<int64_t>(Kw, n - k0);
+        w->tile_pending.push_back(rb_world::TileRun{c0 + k0, K, dt, e, mu, thr, true});
+        w->res_epoch_host += (uint64_t)K + 1;
+        w->res_stats[0] += 1;
+    }
+    w->c += n;
+    w->tile_valid_sp = -1;                           // (the tile bins, if any, are stale)
+    w->primed = false;                               // the hashed forms' table is stale
+    return RB_OK;
+}
+
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
@@ -1267,6 +1605,15 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
     HIPCHK(hipSetDevice(w->device));
+    // the resident form for runs of >= 2 steps (windows chain like tile runs)
+    const bool res = !sharded && res_eligible(w) && nsteps >= 2 && w->tile_pending.size() < 256;
+    if (res && w->res_skip > 0) {
+        --w->res_skip;                               // (back-off after a roll-back: this run steps otherwise)
+    } else if (res) {
+        w->state_version += 1;
+        const int rc = res_run(w, nsteps, dt, e, mu, thr);
+        if (rc != TILE_DECLINED) return rc;          // (declined: the forms below)
+    }
     // the tile form for runs of >= 2 steps, or to continue from its bins;
     // pending tile runs chain (their check waits for the next sync point),
     // anything else first settles them
@@ -1542,7 +1889,7 @@ int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &boun
     const double cs = rmax > 0 ? 4.0 * rmax * 1.001 : 1.0;
     w->inv_cs = 1.0 / cs;
     for (int64_t b = 0; b < w->N; ++b) w->all_spheres = w->all_spheres && d->kind[b] == RB_BODY_SPHERE;
-    HIPCHK(hipMemcpy(w->consts, c.data(), sizeof(T) * c.size(), hipMemcpyHostToDevice));
+    WCHK(wput(w, w->consts, c.data(), sizeof(T) * c.size()));
     // the tile form's constant types: the distinct (m, I) of the bodies, as
     // the arithmetic type holds them (a record carries its type, so the tile
     // kernel reads m and I from a table in LDS instead of by body id)
@@ -1560,13 +1907,13 @@ int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &boun
             for (size_t t = 0; t < types.size(); ++t)
                 for (int k = 0; k < 4; ++k) w->tile_type_val[t][k] = (double)types[t][k];
             HIPCHK(hipMalloc((void **)&w->tile_type_of, (size_t)w->N));
-            HIPCHK(hipMemcpy(w->tile_type_of, type_of.data(), (size_t)w->N, hipMemcpyHostToDevice));
+            WCHK(wput(w, w->tile_type_of, type_of.data(), (size_t)w->N));
             w->tile_ntypes = (int32_t)types.size();
         }
     }
     std::vector<int32_t> k((size_t)w->Npad, 0);
     for (int64_t b = 0; b < w->N; ++b) k[(size_t)b] = d->kind[b];
-    HIPCHK(hipMemcpy(w->kind, k.data(), sizeof(int32_t) * k.size(), hipMemcpyHostToDevice));
+    WCHK(wput(w, w->kind, k.data(), sizeof(int32_t) * k.size()));
     return RB_OK;
 }
 
@@ -1581,7 +1928,8 @@ void free_world(rb_world *w) {
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (w->opt_save) (void)hipFree(w->opt_save);
-    void *tbufs[] = {w->tile_mem, w->tile_fill, w->tile_gen, w->tile_why, w->tile_commits, w->tile_type_of};
+    void *tbufs[] = {w->tile_mem, w->tile_fill, w->tile_gen, w->tile_why, w->tile_commits, w->tile_type_of,
+                     w->res_mem, w->res_epoch};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_host) (void)hipHostFree(w->tile_host);
@@ -1609,7 +1957,7 @@ void free_world(rb_world *w) {
 extern "C" {
 
 const char *rb_last_error(void) { return g_err.c_str(); }
-const char *rb_version(void) { return "librbhip 0.2 (gfx950, HIP)"; }
+const char *rb_version(void) { return "librbhip 0.3 (gfx950, HIP)"; }
 
 int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     ApiScope api_scope_(d ? d->device : -1);
@@ -1676,6 +2024,15 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // from 73,984 up
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_TILE_MIN_BODIES")) w->tile_min_bodies = atoll(ev);
+    // the resident form (rb_resident.hip): RBHIP_RESIDENT = 0 off, 1 every
+    // eligible world, -1 auto (RBHIP_RES_MIN_BODIES .. RBHIP_RES_MAX_BODIES
+    // bodies, retired after RES_MAX_FAILS roll-backs in a row)
+    if (const char *ev = getenv("RBHIP_RESIDENT")) w->res_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
+    if (const char *ev = getenv("RBHIP_RES_MIN_BODIES")) w->res_min_bodies = atoll(ev);
+    if (const char *ev = getenv("RBHIP_RES_MAX_BODIES")) w->res_max_bodies = atoll(ev);
+    if (const char *ev = getenv("RBHIP_RES_WINDOW")) w->res_window = w->res_window_max = std::max(2, std::min(4096, atoi(ev)));
+    if (const char *ev = getenv("RBHIP_RES_REBUILD")) w->res_M = std::max(0, std::min(1000, atoi(ev)));
+    if (const char *ev = getenv("RBHIP_RES_SKIN")) w->res_skin_frac = std::max(0.01, atof(ev));
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
@@ -1768,7 +2125,6 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         for (int k = 0; k < 2; ++k) ALLOC(w->qsnap[k], (size_t)w->esz * 4 * w->Npad);
         ALLOC(w->defer_q, sizeof(int32_t) * (w->S > 0 ? w->S : 1));
         ALLOC(w->defer_cnt, sizeof(int32_t) * 2);
-        if (hipMemset(w->defer_cnt, 0, sizeof(int32_t) * 2) != hipSuccess) return bail(fail(RB_ENODEV, "hipMemset failed"));
     }
     ALLOC(w->state, (size_t)w->esz * 13 * w->S);
     ALLOC(w->consts, (size_t)w->esz * 8 * w->Npad);
@@ -1801,18 +2157,19 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
         hipStreamCreateWithFlags(&w->cap_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(RB_ENODEV, "hipStreamCreate failed"));
     w->stream = w->own_stream;
-    if (hipMemset(w->snap[0], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
-        hipMemset(w->snap[1], 0, (size_t)w->esz * 4 * w->Npad) != hipSuccess ||
-        hipMemset(w->state, 0, (size_t)w->esz * 13 * w->S) != hipSuccess ||
-        // bucket headers of generation 0: every table's generation is >= 2
-        hipMemset(w->ids[0], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
-        hipMemset(w->ids[1], 0, sizeof(uint32_t) * LINE_WORDS * w->H) != hipSuccess ||
-        hipMemset(w->spill[0], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES) != hipSuccess ||
-        hipMemset(w->spill[1], 0, sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES) != hipSuccess ||
-        hipMemset(w->gen, 0, sizeof(uint32_t) * 2) != hipSuccess ||
-        hipMemset(w->err, 0, sizeof(int32_t)) != hipSuccess ||
-        hipStreamSynchronize(nullptr) != hipSuccess)    // (the fills done: NULL_STREAM_DONE)
-        return bail(fail(RB_ENODEV, "hipMemset failed"));
+    {
+        const std::pair<void *, size_t> zero[] = {
+            {w->snap[0], (size_t)w->esz * 4 * w->Npad}, {w->snap[1], (size_t)w->esz * 4 * w->Npad},
+            {w->state, (size_t)w->esz * 13 * w->S},
+            // bucket headers of generation 0: every table's generation is >= 2
+            {w->ids[0], sizeof(uint32_t) * LINE_WORDS * w->H}, {w->ids[1], sizeof(uint32_t) * LINE_WORDS * w->H},
+            {w->spill[0], sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES},
+            {w->spill[1], sizeof(uint32_t) * SPILL_LINE_WORDS * SPILL_LINES},
+            {w->gen, sizeof(uint32_t) * 2}, {w->err, sizeof(int32_t)}, {w->defer_cnt, sizeof(int32_t) * 2}};
+        for (const auto &z : zero)
+            if (z.first && hipMemsetAsync(z.first, 0, z.second, w->stream) != hipSuccess)
+                return bail(fail(RB_ENODEV, "hipMemsetAsync failed"));
+    }
     std::vector<double> bound;
     int rc = w->dtype == RB_F64 ? upload_consts<double>(w, d, bound) : upload_consts<float>(w, d, bound);
     if (rc) return bail(rc);
@@ -1939,6 +2296,8 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     w->primed = false;
     w->tile_valid_sp = -1;
     w->tile_fit_valid = false;                           // (refitted at the next tile run)
+    w->res_fit_valid = false;                            // (and resident run)
+    w->res_declined = false;
     w->state_version += 1;
     // uploading the staging's bytes yields exactly this state (one rank)
     w->mirror_version = w->P == 1 ? w->state_version : -1;
@@ -2012,10 +2371,10 @@ int rb_set_xfrc(rb_world *w, const double *xf) {
     for (int64_t l = 0; l < w->n_local; ++l)
         for (int d = 0; d < 6; ++d) h[(size_t)(d * w->S + l)] = xf[6 * (w->lo + l) + d];
     if (w->dtype == RB_F64) {
-        HIPCHK(hipMemcpy(w->xfrc, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+        WCHK(wput(w, w->xfrc, h.data(), sizeof(double) * h.size()));
     } else {
         std::vector<float> f(h.begin(), h.end());
-        HIPCHK(hipMemcpy(w->xfrc, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice));
+        WCHK(wput(w, w->xfrc, f.data(), sizeof(float) * f.size()));
     }
     return RB_OK;
 }
@@ -2137,8 +2496,8 @@ int rb_p2p_handles(rb_world *w, void *out, int64_t cap, int64_t *len) {
         // kernels poll and read it
         const MailLayout lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
         HIPCHK(hipExtMallocWithFlags((void **)&w->flags, (size_t)lay.bytes, hipDeviceMallocUncached));
-        HIPCHK(hipMemset(w->flags, 0, (size_t)lay.bytes));
-        NULL_STREAM_DONE();
+        WCHK(wfill(w, w->flags, 0, (size_t)lay.bytes));
+        HIPCHK(hipStreamSynchronize(w->stream));     // (the peers map it next)
     }
     hipIpcMemHandle_t h[5];
     HIPCHK(hipIpcGetMemHandle(&h[0], w->snap[0]));
@@ -2159,7 +2518,7 @@ int reset_bounds(rb_world *w) {
     std::vector<int32_t> b((size_t)2 * BOUND_COPIES * BOUND_STRIDE, 0);
     for (int k = 0; k < 2 * BOUND_COPIES; ++k)
         for (int d = 0; d < 3; ++d) { b[(size_t)k * BOUND_STRIDE + d] = INT32_MAX; b[(size_t)k * BOUND_STRIDE + 3 + d] = INT32_MIN; }
-    HIPCHK(hipMemcpy(w->bounds, b.data(), sizeof(int32_t) * b.size(), hipMemcpyHostToDevice));
+    WCHK(wput(w, w->bounds, b.data(), sizeof(int32_t) * b.size()));
     return RB_OK;
 }
 
@@ -2200,19 +2559,18 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len) {
     }
     if (w->boxes) {
         HIPCHK(hipMalloc((void **)&w->peer_quat_dev, sizeof(void *) * quats.size()));
-        HIPCHK(hipMemcpy(w->peer_quat_dev, quats.data(), sizeof(void *) * quats.size(), hipMemcpyHostToDevice));
+        WCHK(wput(w, w->peer_quat_dev, quats.data(), sizeof(void *) * quats.size()));
     }
     HIPCHK(hipMalloc((void **)&w->peer_snap_dev, sizeof(void *) * snaps.size()));
     HIPCHK(hipMalloc((void **)&w->peer_flags_dev, sizeof(int64_t *) * flags.size()));
     HIPCHK(hipMalloc((void **)&w->epoch, sizeof(int64_t)));
-    HIPCHK(hipMemcpy(w->peer_snap_dev, snaps.data(), sizeof(void *) * snaps.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(w->peer_flags_dev, flags.data(), sizeof(int64_t *) * flags.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(w->epoch, 0, sizeof(int64_t)));
-    HIPCHK(hipMemset(w->flags, 0, sizeof(int64_t) * w->P));
-    NULL_STREAM_DONE();
+    WCHK(wput(w, w->peer_snap_dev, snaps.data(), sizeof(void *) * snaps.size()));
+    WCHK(wput(w, w->peer_flags_dev, flags.data(), sizeof(int64_t *) * flags.size()));
+    WCHK(wfill(w, w->epoch, 0, sizeof(int64_t)));
+    WCHK(wfill(w, w->flags, 0, sizeof(int64_t) * w->P));
     // the own cell bounds (both modes filter the peers' bodies by them)
     if (int rc = reset_bounds(w)) return rc;
-    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipStreamSynchronize(w->stream));         // (the flags zeroed before any peer's step can flag)
     w->p2p = true;
     drop_graphs(w);
     return RB_OK;
@@ -2227,8 +2585,7 @@ int rb_p2p_halo(rb_world *w, int32_t enable) {
     if (enable) {
         if (!w->push_cnt) HIPCHK(hipMalloc((void **)&w->push_cnt, sizeof(int32_t) * w->P));
         if (int rc = reset_bounds(w)) return rc;
-        HIPCHK(hipMemset(w->push_cnt, 0, sizeof(int32_t) * w->P));
-        NULL_STREAM_DONE();
+        WCHK(wfill(w, w->push_cnt, 0, sizeof(int32_t) * w->P));
     }
     if (w->halo != (enable != 0)) drop_graphs(w);
     w->halo = enable != 0;
@@ -2252,8 +2609,7 @@ int rb_record_contacts(rb_world *w, int enable) {
         HIPCHK(hipMalloc((void **)&w->rec_partner, sizeof(int32_t) * slots));
         HIPCHK(hipMalloc((void **)&w->rec_kind, sizeof(int32_t) * slots));
         HIPCHK(hipMalloc(&w->rec_dist, (size_t)w->esz * slots));
-        HIPCHK(hipMemset(w->rec_count, 0, sizeof(int32_t) * w->S));
-        NULL_STREAM_DONE();
+        WCHK(wfill(w, w->rec_count, 0, sizeof(int32_t) * w->S));
     }
     if (w->record != (enable != 0)) drop_graphs(w);
     w->record = enable != 0;
@@ -2270,15 +2626,14 @@ int rb_get_contacts(rb_world *w, int32_t *counts, int32_t *partner, int32_t *kin
     const size_t slots = (size_t)w->maxrec * w->S;
     std::vector<int32_t> c((size_t)w->S), pa(slots), ki(slots);
     std::vector<double> di(slots);
-    HIPCHK(hipStreamSynchronize(w->stream));
-    HIPCHK(hipMemcpy(c.data(), w->rec_count, sizeof(int32_t) * w->S, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(pa.data(), w->rec_partner, sizeof(int32_t) * slots, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(ki.data(), w->rec_kind, sizeof(int32_t) * slots, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(c.data(), w->rec_count, sizeof(int32_t) * w->S, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipMemcpyAsync(pa.data(), w->rec_partner, sizeof(int32_t) * slots, hipMemcpyDeviceToHost, w->stream));
+    HIPCHK(hipMemcpyAsync(ki.data(), w->rec_kind, sizeof(int32_t) * slots, hipMemcpyDeviceToHost, w->stream));
     if (w->dtype == RB_F64) {
-        HIPCHK(hipMemcpy(di.data(), w->rec_dist, sizeof(double) * slots, hipMemcpyDeviceToHost));
+        WCHK(wget(w, di.data(), w->rec_dist, sizeof(double) * slots));
     } else {
         std::vector<float> f(slots);
-        HIPCHK(hipMemcpy(f.data(), w->rec_dist, sizeof(float) * slots, hipMemcpyDeviceToHost));
+        WCHK(wget(w, f.data(), w->rec_dist, sizeof(float) * slots));
         for (size_t k = 0; k < slots; ++k) di[k] = f[k];
     }
     int64_t t = 0;
@@ -2372,31 +2727,30 @@ int rb_set_contact_law(rb_world *w, int32_t law, double tol) {
         const size_t bytes = (size_t)w->esz * 8 * w->Npad;
         for (int k = 0; k < 2; ++k) {
             if (hipMalloc(&w->vel[k], bytes) != hipSuccess) return fail(RB_ENOMEM, "hipMalloc(%zu) failed", bytes);
-            HIPCHK(hipMemset(w->vel[k], 0, bytes));
+            WCHK(wfill(w, w->vel[k], 0, bytes));
         }
-        NULL_STREAM_DONE();
     }
     if (w->law == RB_LAW_BALLS && law == RB_LAW_MUJOCO) {
         // the default law keeps positions in the snapshot: restore them
         // from the true positions before the snapshot is read again
         const size_t esz = (size_t)w->esz;
         std::vector<char> st(esz * 13 * w->S), sn(esz * 4 * w->Npad);
-        HIPCHK(hipMemcpy(st.data(), w->state, st.size(), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sn.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(st.data(), w->state, st.size(), hipMemcpyDeviceToHost, w->stream));
+        WCHK(wget(w, sn.data(), w->snap[w->sp()], sn.size()));
         for (int64_t l = 0; l < w->n_local; ++l)
             for (int d = 0; d < 3; ++d)
                 memcpy(&sn[esz * (4 * (w->lo + l) + d)], &st[esz * ((10 + d) * w->S + l)], esz);
-        HIPCHK(hipMemcpy(w->snap[w->sp()], sn.data(), sn.size(), hipMemcpyHostToDevice));
+        WCHK(wput(w, w->snap[w->sp()], sn.data(), sn.size()));
     } else if (w->law == RB_LAW_MUJOCO && law == RB_LAW_BALLS) {
         // the other way: the true positions from the snapshot
         const size_t esz = (size_t)w->esz;
         std::vector<char> st(esz * 13 * w->S), sn(esz * 4 * w->Npad);
-        HIPCHK(hipMemcpy(st.data(), w->state, st.size(), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(sn.data(), w->snap[w->sp()], sn.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(st.data(), w->state, st.size(), hipMemcpyDeviceToHost, w->stream));
+        WCHK(wget(w, sn.data(), w->snap[w->sp()], sn.size()));
         for (int64_t l = 0; l < w->n_local; ++l)
             for (int d = 0; d < 3; ++d)
                 memcpy(&st[esz * ((10 + d) * w->S + l)], &sn[esz * (4 * (w->lo + l) + d)], esz);
-        HIPCHK(hipMemcpy(w->state, st.data(), st.size(), hipMemcpyHostToDevice));
+        WCHK(wput(w, w->state, st.data(), st.size()));
     }
     w->law = law;
     w->tol = tol;
@@ -2419,13 +2773,17 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
+    const bool res = res_eligible(w);
     const bool tile = tile_eligible(w);
-    const int form = tile ? FORM_TILE : step_form(w);
+    const int form = res && w->res_skip == 0 ? FORM_RESIDENT : tile ? FORM_TILE : step_form(w);
     const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), form, w->box_stats[0], w->box_stats[1], w->refits,
                                        w->table_grows, w->H, (int64_t)w->maxp, w->io_stats[0], w->io_stats[1],
                                        w->tile_stats[0], w->tile_stats[1], w->tile_stats[2], w->tile_stats[3],
                                        (int64_t)w->tile_why_seen, (int64_t)w->tile_ntx * w->tile_nty,
-                                       (int64_t)w->tile_tc, tile && w->tile_skip == 0 ? 1 : 0};
+                                       (int64_t)w->tile_tc, tile && w->tile_skip == 0 ? 1 : 0,
+                                       w->res_stats[0], w->res_stats[1], w->res_stats[2], (int64_t)w->res_why_seen,
+                                       (int64_t)w->res_ntx * w->res_nty, res && w->res_skip == 0 ? 1 : 0,
+                                       (int64_t)w->res_window, w->res_stats[3]};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }
@@ -2436,6 +2794,17 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes) {
     if (n_owned) *n_owned = w->n_local;
     if (bytes) *bytes = w->bytes_per_body_step;
     return RB_OK;
+}
+
+int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned) {
+    ApiScope api_scope_(w ? w->device : -1);
+    (void)kmax;
+    (void)band;
+    (void)owned;
+    if (!w) return fail(RB_EINVAL, "null world");
+    if (mode == -1 || mode == 0) return RB_OK;
+    if (mode == 1) return fail(RB_EUNSUPPORTED, "rb_tile_config: the tile blocks were retired (librbhip 0.3)");
+    return fail(RB_EINVAL, "rb_tile_config: mode must be -1, 0 or 1");
 }
 
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches) {

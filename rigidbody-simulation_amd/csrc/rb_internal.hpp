@@ -345,10 +345,70 @@ template <typename T> hipError_t launch_tile_step(const TileParams<T> &p, int ma
 template <typename T> hipError_t launch_tile_build(const TileIO<T> &p, hipStream_t s);   // bins zeroed by the caller
 template <typename T> hipError_t launch_tile_unbin(const TileIO<T> &p, hipStream_t s);
 
+// ---- the resident form (rb_resident.hip) ---------------------------
+// Sphere worlds on one rank.  One launch steps a WINDOW of K reference steps:
+// the plane (x, y) is cut into square tiles of side L mapped periodically
+// onto ntx x nty slots; one single-wave workgroup per slot owns the bodies
+// binned into it at the window start and keeps their state in registers for
+// the whole window.  Each body carries a candidate list (every body within
+// rl in x, y at the last list build, sorted by id) that stays exact while no
+// body moves more than the skin since that build (checked every step); the
+// lists are rebuilt every M steps.  Per step a workgroup reads the positions
+// of the neighbour slots' bodies its lists name ("imports") from the
+// neighbours' publication — 8-byte {tag, half} granules stored write-through,
+// the tag being the step — so a workgroup waits only for its 8 neighbours,
+// never for the grid.  The end state goes to a staging copy that the commit
+// kernel writes into the id-ordered state only if no workgroup failed; any
+// failure raises ERR_TILE with a RES_WHY_* bit and the host replays the window
+// with the hashed forms (the tile form's roll-back, rb_capi.hip tile_finish).
+constexpr int RES_CAP = 64;              // bodies per slot: one wave
+constexpr int RES_LMAX = 20;             // candidates per body's list
+constexpr int RES_MMAX = 112;            // imported neighbour bodies per slot
+constexpr int RES_NU = RES_CAP + RES_MMAX;
+constexpr int RES_STAGE = 9 * RES_CAP;   // bodies of the 3 x 3 slots (list builds)
+enum : int32_t { RES_WHY_LIST = 32, RES_WHY_IMPORT = 64, RES_WHY_SKIN = 128, RES_WHY_DRIFT = 256, RES_WHY_TIMEOUT = 512 };
+template <typename T> struct ResParams {
+    const int32_t *cnt;                  // [slots] bodies binned into each slot
+    const int32_t *ids;                  // [slots][RES_CAP] their ids (bin order)
+    const Snap<T> *snap;                 // the window-start snapshot (id order; state rows and constants: sp)
+    unsigned long long *pub;             // [2][slots][G][RES_CAP] position granules (G = 6 fp64, 3 fp32)
+    Snap<T> *out_snap;                   // [N] the window-end snapshot (staging, id order)
+    T *out_st;                           // [10][S] the window-end q, v, w (staging)
+    StepParams<T> sp;                    // physics, error word, recording (rb_body.hpp)
+    const uint32_t *epoch;               // tag base of this window (the commit kernel advances it)
+    int32_t *abort;                      // set with any failure: spinning workgroups leave
+    int32_t *why;
+    int32_t ntx, nty, K, M;              // slot grid, steps, list-rebuild period (>= K: never)
+    T L, inv_L;                          // tile side
+    T rl;                                // list radius in x, y
+    T skin2;                             // squared x, y displacement allowed since a list build
+    T drift;                             // distance a body may leave its home tile (rebuilding windows)
+    int32_t rec;                         // record the window's last step
+    int64_t timeout;                     // s_memrealtime ticks (100 MHz) a wait may spin
+};
+template <typename T> struct ResCommit {
+    const int32_t *err;
+    const Snap<T> *out_snap;
+    const T *out_st;
+    Snap<T> *snap;                       // the id-ordered snapshot of the window-end step parity
+    BodyState<T> st;
+    int64_t n, S;
+    uint32_t *epoch;                     // += K + 1 (the next window's tags lie above this one's)
+    int32_t K;
+    int32_t *abort;                      // cleared
+    unsigned long long *commits;         // += 1 when the window committed
+};
+template <typename T> hipError_t launch_res_bin(const ResParams<T> &p, int64_t n, hipStream_t s);   // cnt zeroed by the caller
+template <typename T> hipError_t launch_res_step(const ResParams<T> &p, int maxp, hipStream_t s);
+template <typename T> hipError_t launch_res_commit(const ResCommit<T> &p, hipStream_t s);
+// workgroups of the resident kernel one CU holds (its LDS and registers)
+int res_blocks_per_cu(int dtype_f64, int maxp);
+
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one
 // lane per body at one wave per SIMD (mid-size scenes)
-enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4, FORM_TILE = 5 };
+enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4, FORM_TILE = 5,
+             FORM_RESIDENT = 6 };
 // boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
 // the wide form's kernel alone (its own translation unit: scheduled for memory clauses)

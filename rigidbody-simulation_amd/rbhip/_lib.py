@@ -74,15 +74,18 @@ SIGNATURES = {
     "rb_set_contact_law": (C.c_int, [_P, _I32, _D]),
     "rb_query": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64)]),
     "rb_kernel_timing": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(_I64)]),
+    "rb_tile_config": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_double, _I64]),
     "rb_world_stats": (C.c_int, [_P, C.POINTER(_I64), _I32]),
 }
 
 # rb_world_stats indices (include/rbhip.h RB_STAT_*)
 STAT_NAMES = ["graphs", "form", "box_opt_chunks", "box_rollbacks", "refits", "table_grows", "buckets",
               "max_partners", "io_skipped", "io_uploads", "tile_runs", "tile_steps", "tile_rollbacks",
-              "tile_builds", "tile_why", "tile_slots", "tile_cols", "tile_on"]
+              "tile_builds", "tile_why", "tile_slots", "tile_cols", "tile_on", "res_windows", "res_steps",
+              "res_rollbacks", "res_why", "res_slots", "res_on", "res_window", "res_fits"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
-              3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help", 5: "rb::tile_step_kernel"}
+              3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help", 5: "rb::tile_step_kernel",
+              6: "rb::res_step_kernel"}
 
 _lib = None
 

@@ -191,30 +191,41 @@ def body_index(model, obj: str) -> int:
 
 def step_model(model, data, nsteps: int, dt: float, restitution: float, friction: float,
                threshold: float, normal_convention: str = "oriented", law: str = "mujoco",
-               tol: float = 0.01) -> None:
+               tol: float = 0.01, only: Optional[int] = None) -> None:
     """Upload data's state, run nsteps reference steps on the GPU, write back
-    (the free bodies' joints only, at their jnt_qposadr / jnt_dofadr)."""
+    (the free bodies' joints only, at their jnt_qposadr / jnt_dofadr).
+
+    only = k: the single-body entries on a scene of several free bodies
+    (time_integeration.py:13-72, collision.py:56-102; SURVEY D11 "with N
+    bodies, filter by body"): one step of free body k alone — its gravity,
+    its own contacts (planes, then partners by ascending id, the partners
+    static at their step-start positions) and its integration; every other
+    body stays where it is.  The device steps every body (a step is Jacobi
+    across bodies, so the others' results never feed body k's) and only
+    body k's rows are written back: an owned-body mask at the boundary."""
     w = world_for(model, normal_convention, law, tol, restitution, friction)
     qi, vi, fb, contiguous = _layout(model, w)
     qpos, qvel = np.asarray(data.qpos), np.asarray(data.qvel)
     n = fb.shape[0]
+    if only is not None:
+        if not 0 <= only < n:
+            raise ValueError(f"free body {only} out of range (0..{n - 1})")
+        if nsteps != 1:
+            raise ValueError("a single-body step is one reference step")
+        w.set_state(qpos[qi], qvel[vi])
+        w.set_xfrc(_applied(data, fb))
+        w.step(1, dt=dt, restitution=restitution, friction=friction, threshold=threshold)
+        q, v = w.get_state()
+        data.qpos[qi[only]] = q[only]
+        data.qvel[vi[only]] = v[only]
+        return
     contiguous = contiguous and all(isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous
                                     for a in (data.qpos, data.qvel))
     if contiguous:                  # free joints at qpos[0:7n] / qvel[0:6n]: views, no gathers
         w.set_state(qpos[:7 * n].reshape(n, 7), qvel[:6 * n].reshape(n, 6))
     else:
         w.set_state(qpos[qi], qvel[vi])
-    # applied forces (collision.py:66-70): the common all-zero array is told
-    # by one contiguous scan, without gathering the free bodies' rows
-    xf = getattr(data, "xfrc_applied", None)
-    xf_free = None
-    if xf is not None:
-        xf = np.asarray(xf)
-        if xf.shape[0] > fb[-1] and not _all_zero(xf):
-            xf_free = xf[fb]
-            if not np.any(xf_free):
-                xf_free = None
-    w.set_xfrc(xf_free)
+    w.set_xfrc(_applied(data, fb))
     w.step(nsteps, dt=dt, restitution=restitution, friction=friction, threshold=threshold)
     if contiguous:
         w.get_state(data.qpos[:7 * n].reshape(n, 7), data.qvel[:6 * n].reshape(n, 6))
@@ -222,6 +233,20 @@ def step_model(model, data, nsteps: int, dt: float, restitution: float, friction
         q, v = w.get_state()
         data.qpos[qi] = q
         data.qvel[vi] = v
+
+
+def _applied(data, fb):
+    """The free bodies' applied forces (collision.py:66-70), or None when
+    all zero: the common all-zero array is told by one contiguous scan,
+    without gathering the free bodies' rows."""
+    xf = getattr(data, "xfrc_applied", None)
+    if xf is None:
+        return None
+    xf = np.asarray(xf)
+    if xf.shape[0] <= fb[-1] or _all_zero(xf):
+        return None
+    xf_free = xf[fb]
+    return xf_free if np.any(xf_free) else None
 
 
 def _all_zero(a: np.ndarray) -> bool:

@@ -52,9 +52,10 @@ def custom_step_with_impulse_collision_friction(model, obj, data, dt=0.01, resti
     integration.  Mutates data.qpos[0:7] / data.qvel[0:6]; returns the new
     position (3,)."""
     k = adapter.body_index(model, obj)
-    n = len(np.asarray(data.qpos)) // 7
-    if n != 1 or k != 0:
-        raise ValueError("single-body step on a scene with several free bodies: use "
-                         "src.simulation.multi_sphere_bounce.custom_step_multi_sphere")
-    adapter.step_model(model, data, 1, dt, restitution, friction_coeff, contact_threshold)
-    return np.array(data.qpos[0:3], dtype=np.float64)
+    n = len(adapter.free_bodies(model))
+    # several free bodies: body k alone steps, its contacts filtered by body
+    # (SURVEY D11; the reference applies every contact to the one body)
+    adapter.step_model(model, data, 1, dt, restitution, friction_coeff, contact_threshold,
+                       only=k if n > 1 else None)
+    qi, _ = adapter.state_index(model)
+    return np.array(np.asarray(data.qpos)[qi[k, 0:3]], dtype=np.float64)

@@ -132,3 +132,35 @@ def test_simulate_multi_sphere_vs_oracle(oracle):
     q, v, logger = simulate.run("multi_sphere", 250, log_every=50)
     assert np.array_equal(q, qo) and np.array_equal(v, vo)
     assert len(logger.loggers["ball1"].times) == 5
+
+
+@pytest.mark.parametrize("entry", ["timestep_integration", "custom_step_with_impulse_collision_friction"])
+def test_single_body_entry_on_multi_body_scene(oracle, entry):
+    """time_integeration.py:13-72 / collision.py:56-102 called for one named
+    body of a scene with several (contacts filtered by body):
+    that body alone steps — gravity, its plane and partner contacts against
+    the others' step-start positions, integration — and the others stay
+    put.  Checked bit for bit against the oracle stepping the same body
+    (the oracle steps all, then keeps only that body's row)."""
+    from rbhip import adapter
+    import src.physics.collision as col
+    import src.physics.time_integeration as ti
+    g = load_golden("traj_flat64")
+    sc = golden_scene(g)
+    names = [f"ball{k}" for k in range(sc.n)]
+    sc = sc.with_(names=names)
+    model, data = adapter.load_scene_model(sc)
+    fn = getattr(ti if entry == "timestep_integration" else col, entry)
+    osc = oracle.OracleScene(sc)
+    q, v = sc.qpos0.copy(), sc.qvel0.copy()
+    rng = np.random.default_rng(3)
+    thr = 1e-4 if entry == "timestep_integration" else 0.0
+    for t in range(160):
+        k = int(rng.integers(sc.n)) if t % 4 else 5      # body 5 often: it lands and touches neighbours
+        pos = fn(model, names[k], data, dt=sc.dt, restitution=sc.restitution, friction_coeff=sc.friction,
+                 contact_threshold=thr)
+        q1, v1 = oracle.step(osc, q, v, 1, dt=sc.dt, restitution=sc.restitution, friction=sc.friction, threshold=thr)
+        q[k], v[k] = q1[k], v1[k]
+        assert np.array_equal(pos, q[k, 0:3])
+        assert np.array_equal(np.asarray(data.qpos).reshape(-1, 7), q), f"qpos differs after call {t}"
+        assert np.array_equal(np.asarray(data.qvel).reshape(-1, 6), v), f"qvel differs after call {t}"

@@ -59,6 +59,25 @@ def test_single_sphere_reproduces_reference_plot():
     assert abs(g["qpos"][k, 0] - 0.62) < 0.03 and abs(g["qpos"][k, 1] + 0.62) < 0.03
 
 
+def test_single_cube_reproduces_reference_plot():
+    """data/plots/cube/cube_height_vs_time.png: the cube of
+    config 5 (cube_incline.py via timestep_integration, time_integeration.py:13-72;
+    dt 0.009, e 0.2, mu 0.6, threshold 1e-4) slides down the 0.7 rad incline,
+    its height z read off the reference's committed plot at
+    (t, z) = (0.495, 0.207), (0.999, -0.290), (1.494, -1.068), (1.998, -2.155),
+    (2.133, -2.497) — the plot ends near -2.47 at about 2.13 s.  Tolerance
+    0.03: the plot-reading precision.  This pins the restated plane-box
+    contact rule (MuJoCo's mjc_PlaneBox, unavailable offline) that C5 uses."""
+    g = load_golden("traj_single_cube")
+    dt = float(g["params"][0])
+    z = g["qpos"][:, 2]
+    for t, want in [(0.495, 0.207), (0.999, -0.290), (1.494, -1.068), (1.998, -2.155), (2.133, -2.497)]:
+        k = int(round(t / dt))
+        assert abs(z[k] - want) <= 0.03, (t, z[k], want)
+    # and the cube keeps sliding (no rest) over the plotted range
+    assert np.all(np.diff(z[int(round(0.5 / dt)):int(round(2.13 / dt))]) < 0)
+
+
 @pytest.mark.parametrize("name", NBODY_GOLDENS)
 def test_nbody_trajectory_and_contacts_bit_exact(oracle, name):
     g = load_golden(name)
