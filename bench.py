@@ -301,21 +301,37 @@ class SingleWorldCheck:
 
 
 def step_kernel_name(stats: dict) -> str:
-    """The kernel that stepped the timed region, as the library reports it
-    (rb_world_stats "form")."""
+    """The kernel of a form (rb_world_stats "form" numbering)."""
     from rbhip import _lib
     return _lib.FORM_NAMES.get(stats.get("form"), "?")
 
 
-def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str, tile: bool = False):
+def region_form(st0: dict, st1: dict, steps: int):
+    """(form, clean) of the timed region, from the counters before and after
+    it: the resident or tile form only if it committed every one of the K
+    steps with no roll-back; a roll-back inside the region (its steps then
+    replayed by the hashed forms) makes the region mixed (clean False: its
+    kernel time is not one form's); otherwise the hashed form the world
+    steps with."""
+    d = lambda k: st1.get(k, 0) - st0.get(k, 0)   # noqa: E731
+    if d("res_rollbacks") or d("tile_rollbacks"):
+        return st1.get("hashed_form", st1.get("form")), False
+    if d("res_steps") == steps:
+        return 6, True
+    if d("tile_steps") == steps:
+        return 5, True
+    return st1.get("hashed_form", st1.get("form")), True
+
+
+def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str, suffix: str = ""):
     """(upper, lower, source) HBM bytes per step-kernel launch from the
     committed PMC summary (profiles/pmc_traffic.json, profiles/collect_pmc.py);
     keyed by config and dtype for one GPU, with a _p<N> suffix for strong
-    shards and _tile when the tile form stepped the timed region.  (None,
+    shards and _tile / _res when the tile / resident form stepped the timed region.  (None,
     None, None) when that shape was never collected."""
     rel = os.path.join("profiles", "pmc_traffic.json")
     key = f"{cfg}_{dtype}" if P == 1 or scaling == "weak" else f"{cfg}_{dtype}_p{P}"
-    key += "_tile" if tile else ""
+    key += suffix
     try:
         with open(os.path.join(ROOT, rel)) as f:
             e = json.load(f).get(key)
@@ -457,8 +473,15 @@ def main():
         timing = "HIP event pair around each step-kernel launch (second run of K steps)"
     bytes_per_launch = w.bytes_per_body_step * w.n_owned
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, traffic_lower, traffic_src, traffic_same_build = traffic_from_profiles(args.config, args.dtype, P,
-                                                                                    args.scaling, st1.get("form") == 5)
+    form, clean = region_form(st0, st1, args.steps) if P == 1 else (st1.get("hashed_form", st1.get("form")), True)
+    traffic, traffic_lower, traffic_src, traffic_same_build = traffic_from_profiles(
+        args.config, args.dtype, P, args.scaling, {5: "_tile", 6: "_res"}.get(form, ""))
+    if form == 6:
+        timing += (f"; the resident form steps a window of {st1.get('res_window')} steps per launch: "
+                   f"avg_launch_ms and algorithmic_bytes_per_launch are per step")
+    if not clean:
+        traffic = traffic_lower = traffic_src = None
+        timing += "; MIXED region: a roll-back inside it was replayed by the hashed forms"
 
     value = scene.n * args.steps / elapsed
     line = {
@@ -486,10 +509,11 @@ def main():
                        "exchange_probe_ms_per_step": probes} if P > 1 else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_lower": traffic_lower,
+                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE / WRITE_SIZE; upper and lower bound)",
                      "traffic_source": traffic_src,
                      # the counters were collected on this very library build
                      "traffic_same_build": traffic_same_build,
-                     "kernel": step_kernel_name(st1),
+                     "kernel": step_kernel_name({"form": form}),
                      "avg_launch_ms": avg_ms, "launches_timed": launches,
                      "timing": timing,
                      "algorithmic_bytes_per_launch": bytes_per_launch},

@@ -285,7 +285,7 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
  * ABI note: librbhip 0.3 (rb_version) renumbered the counters of 0.2 — the
  * round-4 block counters were removed and RB_STAT_FORM, _BUCKETS,
  * _MAX_PARTNERS and _IO_* moved (8 -> 1, 19 -> 6, 20 -> 7, 27/28 -> 8/9;
- * RB_STATS_COUNT 30 -> 18, then 26 with the resident counters appended).  A
+ * RB_STATS_COUNT 30 -> 18, then 27 with the resident counters appended).  A
  * consumer built against the 0.2 header must be rebuilt; from 0.3 on new
  * counters are only appended. */
 #define RB_STAT_GRAPHS          0   /* captured step graphs alive               */
@@ -319,7 +319,9 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
 #define RB_STAT_RES_ON         23   /* the next run of >= 2 steps would use the resident form */
 #define RB_STAT_RES_WINDOW     24   /* steps per resident window now */
 #define RB_STAT_RES_FITS       25   /* resident tilings fitted */
-#define RB_STATS_COUNT         26
+#define RB_STAT_HASHED_FORM    26   /* the hashed-cell form (0-4, as RB_STAT_FORM) the world steps with when
+                                       neither the tile nor the resident form does */
+#define RB_STATS_COUNT         27
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

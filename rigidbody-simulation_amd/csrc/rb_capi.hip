@@ -340,12 +340,15 @@ struct rb_world {
     int64_t res_min_bodies = 4097, res_max_bodies = 131072;
     bool res_fit_valid = false;
     bool res_declined = false;     // the fit found no tiling (a slot over its capacity, or too many slots)
-    double res_L = 0, res_rl = 0, res_skin = 0, res_drift = 0;
-    double res_skin_frac = 1.0;    // skin = this x the largest contact reach (RBHIP_RES_SKIN)
-    int32_t res_ntx = 0, res_nty = 0;
-    int32_t res_window = 64;       // steps per window (halved after a skin / drift failure, grown back on success)
-    int32_t res_window_max = 64;   // RBHIP_RES_WINDOW
-    int32_t res_M = 8;             // list rebuild period (RBHIP_RES_REBUILD; 0: never within a window)
+    double res_L = 0, res_R = 0, res_ox = 0, res_oy = 0;   // tile side, export band, grid origin
+    int32_t res_ntx = 0, res_nty = 0, res_ncx = 0;
+    double res_fill = 0.7;         // the fit's largest tile occupancy / RES_CAP (RBHIP_RES_FILL)
+    int32_t res_window = 512;      // steps per window (one launch)
+    int32_t res_window_max = 512;  // RBHIP_RES_WINDOW
+    // constants by type (ResParams::types): <= RES_TYPES distinct (m, I, r), else no resident form
+    int32_t res_ntypes = 0;
+    double res_type_val[RES_TYPES][5] = {};
+    uint8_t *res_type_of = nullptr;  // [N]
     int64_t res_max_slots = 0;     // slots the GPU holds resident at once (with a margin)
     void *res_mem = nullptr;       // counts, ids, publication, staging
     size_t res_mem_bytes = 0;
@@ -1282,7 +1285,6 @@ int tile_finish(rb_world *w) {
         // committed windows: the form works on this scene (grow the window back)
         w->res_fails = 0;
         if (w->res_backoff > 0) w->res_backoff /= 2;
-        w->res_window = std::min(w->res_window_max, 2 * w->res_window);
     }
     if (!(err & ERR_TILE)) {
         if (w->tile_backoff > 0) w->tile_backoff /= 2;
@@ -1308,8 +1310,9 @@ int tile_finish(rb_world *w) {
         // form after RES_MAX_FAILS roll-backs in a row.
         w->res_stats[2] += 1;
         w->res_why_seen |= why;
-        if (why & (RES_WHY_SKIN | RES_WHY_DRIFT)) w->res_window = std::max(4, w->res_window / 2);
-        if (why & (TILE_WHY_CAP | RES_WHY_LIST | RES_WHY_IMPORT)) w->res_fit_valid = false;
+        // a body left the grid, or a slot / publication / import table
+        // overflowed: a new fit from the positions the replay reaches
+        if (why & (RES_WHY_GRID | TILE_WHY_CAP | RES_WHY_IMPORT | RES_WHY_PUB)) w->res_fit_valid = false;
         w->res_backoff = w->res_backoff ? std::min(2 * w->res_backoff, 64) : 1;
         w->res_skip = w->res_backoff;
         if (++w->res_fails >= RES_MAX_FAILS && w->res_mode == -1) w->res_mode = 0;
@@ -1342,7 +1345,7 @@ bool res_eligible(const rb_world *w) {
     if (w->res_mode == 0 || w->res_declined || w->tile_replaying || w->P != 1 || !w->all_spheres ||
         w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
         return false;
-    if (w->maxp > 32 || w->n_local <= 0 || w->N >= (int64_t)1 << 30) return false;
+    if (w->maxp > 32 || w->n_local <= 0 || w->N >= (int64_t)1 << RES_ID_BITS || w->res_ntypes < 1) return false;
     return w->res_mode == 1 || (w->n_local >= w->res_min_bodies && w->n_local <= w->res_max_bodies);
 }
 
@@ -1358,38 +1361,38 @@ int64_t res_capacity(rb_world *w) {
 }
 
 // The tiling from body positions (x, y at pos[k * stride], pos[k * stride + 1]):
-// skin = res_skin_frac x the largest contact reach, list radius rl = reach +
-// 2 skin; the largest tile side L >= 1.5 rl (a drift room of rl / 4 per side
-// for windows that rebuild their lists) whose fullest tile holds at most 7/8
-// of a slot; ntx x nty slots over the scene's extent plus one ring.  A scene
-// no tiling fits (a tile over capacity at the smallest side, or more slots
-// than the GPU holds resident) is declined until its next rb_set_state.
+// the export band R = the largest contact reach (2 rmax, with a margin), the
+// search cell 2 R; the largest tile side L in [3 R, (RES_CELLS^1/2 - 1) 2 R - 2 R]
+// whose fullest tile holds at most res_fill x RES_CAP bodies (room for the
+// bodies that move in before the next fit); the grid covers the scene's
+// extent plus a ring of one tile.  A scene no tiling fits (a tile over that
+// occupancy at the smallest side, or more slots than the GPU holds resident)
+// is declined until its next rb_set_state.
 void res_fit(rb_world *w, const double *pos, int64_t stride) {
     w->res_stats[3] += 1;
     w->res_fit_valid = true;
     w->res_declined = false;
-    const double reach = 2.0 * w->rmax;
-    w->res_skin = w->res_skin_frac * reach;
-    w->res_rl = reach + 2.0 * w->res_skin;
+    const double R = 2.0 * w->rmax * (1.0 + 1e-6) + 1e-12;
+    const double cs = 2.0 * R * (1.0 + 1e-6);
     std::vector<double> xs, ys;
     xs.reserve((size_t)w->N);
     ys.reserve((size_t)w->N);
     double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
     for (int64_t b = 0; b < w->N; ++b) {
         const double x = pos[b * stride], y = pos[b * stride + 1];
-        if (!(fabs(x) < 1e9 && fabs(y) < 1e9)) continue;
+        if (!(fabs(x) < 1e9 && fabs(y) < 1e9)) { w->res_declined = true; return; }
         xs.push_back(x);
         ys.push_back(y);
         lo[0] = std::min(lo[0], x); hi[0] = std::max(hi[0], x);
         lo[1] = std::min(lo[1], y); hi[1] = std::max(hi[1], y);
     }
     if (xs.empty()) { w->res_declined = true; return; }
-    const int64_t limit = 7 * RES_CAP / 8;
+    const int64_t limit = std::max<int64_t>(1, (int64_t)(w->res_fill * RES_CAP));
     std::vector<int64_t> t(xs.size());
     auto worst = [&](double L) {
         const double inv = 1.0 / L;
         for (size_t k = 0; k < xs.size(); ++k)
-            t[k] = (((int64_t)floor(xs[k] * inv) + (1 << 30)) << 31) | ((int64_t)floor(ys[k] * inv) + (1 << 30));
+            t[k] = (((int64_t)floor((xs[k] - lo[0]) * inv)) << 31) | (int64_t)floor((ys[k] - lo[1]) * inv);
         std::sort(t.begin(), t.end());
         int64_t m = 0;
         for (size_t a = 0; a < t.size();) {
@@ -1400,31 +1403,37 @@ void res_fit(rb_world *w, const double *pos, int64_t stride) {
         }
         return m;
     };
-    const double Lmin = w->res_rl * 1.5;
-    if (worst(Lmin) > limit) { w->res_declined = true; return; }
+    const int side = (int)floor(sqrt((double)RES_CELLS));
+    const double Lmin = 3.0 * R, Lmax = (side - 1) * cs - 2.0 * R;
+    if (Lmax < Lmin || worst(Lmin) > limit) { w->res_declined = true; return; }
     double L = Lmin;
-    while (L < 1e6 && worst(L * 1.25) <= limit) L *= 1.25;
+    while (L * 1.25 <= Lmax && worst(L * 1.25) <= limit) L *= 1.25;
     for (int k = 0; k < 6; ++k) {                    // (bisect the last factor)
         const double mid = L * (1.0 + 0.25 / (2 << k));
-        if (worst(mid) <= limit) L = mid;
+        if (mid <= Lmax && worst(mid) <= limit) L = mid;
     }
-    const int64_t ntx = (int64_t)floor(hi[0] / L) - (int64_t)floor(lo[0] / L) + 3;
-    const int64_t nty = (int64_t)floor(hi[1] / L) - (int64_t)floor(lo[1] / L) + 3;
+    // the grid: the extent's tiles plus a ring of one (origin on a multiple of L)
+    const double ox = (floor(lo[0] / L) - 1.0) * L, oy = (floor(lo[1] / L) - 1.0) * L;
+    const int64_t ntx = (int64_t)floor((hi[0] - ox) / L) + 2, nty = (int64_t)floor((hi[1] - oy) / L) + 2;
     if (ntx * nty > res_capacity(w) || ntx * nty > INT32_MAX / (8 * RES_CAP)) { w->res_declined = true; return; }
     w->res_L = L;
-    w->res_ntx = (int32_t)std::max<int64_t>(3, ntx);
-    w->res_nty = (int32_t)std::max<int64_t>(3, nty);
-    w->res_drift = 0.5 * (L - w->res_rl) * (1.0 - 1e-6);
+    w->res_R = R;
+    w->res_ox = ox;
+    w->res_oy = oy;
+    w->res_ntx = (int32_t)ntx;
+    w->res_nty = (int32_t)nty;
+    w->res_ncx = (int32_t)ceil((L + 2.0 * R) / cs) + 1;
+    if (w->res_ncx * w->res_ncx > RES_CELLS) { w->res_declined = true; return; }
 }
 
 size_t res_bytes(const rb_world *w, size_t *o_ids, size_t *o_pub, size_t *o_snap, size_t *o_st) {
-    const size_t slots = (size_t)w->res_ntx * w->res_nty, esz = (size_t)w->esz, G = w->dtype == RB_F64 ? 6 : 3;
+    const size_t slots = (size_t)w->res_ntx * w->res_nty, esz = (size_t)w->esz;
     auto up = [](size_t v) { return (v + 255) / 256 * 256; };
     size_t o = up(slots * 4);
     *o_ids = o;
     o += up(slots * RES_CAP * 4);
     *o_pub = o;
-    o += up(2 * slots * G * RES_CAP * 8);
+    o += up(2 * slots * RES_PUB_WORDS * 8);
     *o_snap = o;
     o += up((size_t)w->Npad * 4 * esz);
     *o_st = o;
@@ -1484,13 +1493,16 @@ template <typename T> ResParams<T> make_res(rb_world *w, int64_t c0, int32_t K, 
     p.ntx = w->res_ntx;
     p.nty = w->res_nty;
     p.K = K;
-    p.M = w->res_M > 0 && w->res_M < K ? w->res_M : 0;
+    p.ox = (T)w->res_ox;
+    p.oy = (T)w->res_oy;
     p.L = (T)w->res_L;
     p.inv_L = (T)(1.0 / w->res_L);
-    p.rl = (T)w->res_rl;
-    const double sk = w->res_skin * (1.0 - 1e-6);
-    p.skin2 = (T)(sk * sk);
-    p.drift = (T)w->res_drift;
+    p.R = (T)w->res_R;
+    p.inv_cs = (T)(1.0 / (2.0 * w->res_R * (1.0 + 1e-6)));
+    p.ncx = w->res_ncx;
+    p.type_of = w->res_type_of;
+    for (int t = 0; t < RES_TYPES; ++t)
+        for (int k = 0; k < 5; ++k) p.types[t][k] = (T)w->res_type_val[t][k];
     p.rec = rec ? 1 : 0;
     p.timeout = 5000000;                             // 50 ms of s_memrealtime (100 MHz)
     return p;
@@ -1567,7 +1579,7 @@ int res_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) 
         return RB_OK;
     }
     const int64_t c0 = w->c;
-    const int variant = 16 | 64 | (int)w->record | (Kw << 8) | (w->res_M << 20);
+    const int variant = 16 | 64 | (int)w->record | (Kw << 8);
     int rc = graph_replay(w, n, variant, dt, e, mu, thr, [&](hipStream_t s, int64_t cs) {
         for (int64_t k0 = 0; k0 < n; k0 += Kw) {
             const int32_t K = (int32_t)std::min<int64_t>(Kw, n - k0);
@@ -1911,6 +1923,27 @@ int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &boun
             w->tile_ntypes = (int32_t)types.size();
         }
     }
+    // the resident form's constant types: distinct (m, ix, iy, iz, r) as the
+    // arithmetic type holds them (a migrant or export carries its type)
+    {
+        std::vector<std::array<T, 5>> types;
+        std::vector<uint8_t> type_of((size_t)w->N, 0);
+        for (int64_t b = 0; b < w->N && types.size() <= (size_t)RES_TYPES; ++b) {
+            const std::array<T, 5> t = {(T)d->mass[b], (T)d->inertia[3 * b], (T)d->inertia[3 * b + 1],
+                                        (T)d->inertia[3 * b + 2], (T)bound[(size_t)b]};
+            size_t k = 0;
+            while (k < types.size() && memcmp(types[k].data(), t.data(), sizeof(t)) != 0) ++k;
+            if (k == types.size()) types.push_back(t);
+            type_of[(size_t)b] = (uint8_t)k;
+        }
+        if (types.size() <= (size_t)RES_TYPES) {
+            for (size_t t = 0; t < types.size(); ++t)
+                for (int k = 0; k < 5; ++k) w->res_type_val[t][k] = (double)types[t][k];
+            HIPCHK(hipMalloc((void **)&w->res_type_of, (size_t)w->N));
+            WCHK(wput(w, w->res_type_of, type_of.data(), (size_t)w->N));
+            w->res_ntypes = (int32_t)types.size();
+        }
+    }
     std::vector<int32_t> k((size_t)w->Npad, 0);
     for (int64_t b = 0; b < w->N; ++b) k[(size_t)b] = d->kind[b];
     WCHK(wput(w, w->kind, k.data(), sizeof(int32_t) * k.size()));
@@ -1929,7 +1962,7 @@ void free_world(rb_world *w) {
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (w->opt_save) (void)hipFree(w->opt_save);
     void *tbufs[] = {w->tile_mem, w->tile_fill, w->tile_gen, w->tile_why, w->tile_commits, w->tile_type_of,
-                     w->res_mem, w->res_epoch};
+                     w->res_mem, w->res_epoch, w->res_type_of};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_host) (void)hipHostFree(w->tile_host);
@@ -2031,8 +2064,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     if (const char *ev = getenv("RBHIP_RES_MIN_BODIES")) w->res_min_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_RES_MAX_BODIES")) w->res_max_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_RES_WINDOW")) w->res_window = w->res_window_max = std::max(2, std::min(4096, atoi(ev)));
-    if (const char *ev = getenv("RBHIP_RES_REBUILD")) w->res_M = std::max(0, std::min(1000, atoi(ev)));
-    if (const char *ev = getenv("RBHIP_RES_SKIN")) w->res_skin_frac = std::max(0.01, atof(ev));
+    if (const char *ev = getenv("RBHIP_RES_FILL")) w->res_fill = std::max(0.1, std::min(1.0, atof(ev)));
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
@@ -2783,7 +2815,7 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
                                        (int64_t)w->tile_tc, tile && w->tile_skip == 0 ? 1 : 0,
                                        w->res_stats[0], w->res_stats[1], w->res_stats[2], (int64_t)w->res_why_seen,
                                        (int64_t)w->res_ntx * w->res_nty, res && w->res_skip == 0 ? 1 : 0,
-                                       (int64_t)w->res_window, w->res_stats[3]};
+                                       (int64_t)w->res_window, w->res_stats[3], step_form(w)};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

@@ -1,9 +1,9 @@
 """Diagnostic: per-step stamps of the resident kernel (diag/res_stamps.so,
 built with EXTRA=-DRB_RES_STAMPS=1).  Steps a scene in the resident form,
 then one more window of K steps, and prints from the constant 100 MHz clock:
-the launch's start spread, each workgroup's setup (list build), and per step
-the time to the imports' arrival and to the publication (median / p90 /
-max over the slots), relative to the launch's first start.  Not part of the
+the launch's start spread, each workgroup's setup, and per step the time to
+the imports' arrival, the cell sort, the solve and the publication (median /
+p90 / max over the slots), relative to the launch's first start.  Not part of the
 product.
 
     python scripts/res_stamps.py [--config c2] [--warm 40] [--k 16] [--lib diag/res_stamps.so]
@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--warm", type=int, default=40)
-    ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--lib", default=os.path.join(ROOT, "diag", "res_stamps.so"))
     a = ap.parse_args()
     import numpy as np
@@ -57,11 +57,24 @@ def main():
     print(f"{a.config}: {nb} slots, {int(live.sum())} with bodies; K = {a.k}; stats {st}")
     print(f"  (us after the first start: median p90 max)")
     print(f"  start                  {q(us(s[:, 0]))}")
-    print(f"  setup done (list build) {q(us(s[:, 1]))}")
-    for t in range(min(a.k, 16)):
-        print(f"  step {t:2d} imports in    {q(us(s[:, 4 + 2 * t]))}   published {q(us(s[:, 5 + 2 * t]))}")
+    print(f"  setup done (bin lists)  {q(us(s[:, 1]))}")
+    n = min(a.k, 8)
+    for t in range(n):
+        c = 4 + 4 * t
+        print(f"  step {t}: imports in {q(us(s[:, c]))} | sorted {q(us(s[:, c + 1]))} | "
+              f"solved {q(us(s[:, c + 2]))} | published {q(us(s[:, c + 3]))}")
     print(f"  end                    {q(us(s[:, 2]))}")
-    d = np.diff(np.median(us(s[:, 5:5 + 2 * min(a.k, 16):2]), axis=0))
+    # per phase (median over slots of each slot's own interval), steps 1 .. n-2
+    ph = {"wait + import": [], "cell sort": [], "solve": [], "export + publish": []}
+    for t in range(1, n - 1):
+        c = 4 + 4 * t
+        ph["wait + import"].append(np.median(s[:, c] - s[:, c - 1]) / 100.0)
+        ph["cell sort"].append(np.median(s[:, c + 1] - s[:, c]) / 100.0)
+        ph["solve"].append(np.median(s[:, c + 2] - s[:, c + 1]) / 100.0)
+        ph["export + publish"].append(np.median(s[:, c + 3] - s[:, c + 2]) / 100.0)
+    for k, v in ph.items():
+        print(f"  phase {k:18s} median over slots, per step: {np.round(v, 2).tolist()}")
+    d = np.diff(np.median(us(s[:, 7:4 + 4 * n:4]), axis=0))
     print(f"  per step (median publication to publication): {np.round(d, 2).tolist()}")
 
 
