@@ -308,16 +308,14 @@ def step_kernel_name(stats: dict) -> str:
 
 def region_form(st0: dict, st1: dict, steps: int):
     """(form, clean) of the timed region, from the counters before and after
-    it: the resident or tile form only if it committed every one of the K
-    steps with no roll-back; a roll-back inside the region (its steps then
+    it: the tile form only if it committed every one of the K steps with no
+    roll-back; a roll-back inside the region (its steps then
     replayed by the hashed forms) makes the region mixed (clean False: its
     kernel time is not one form's); otherwise the hashed form the world
     steps with."""
     d = lambda k: st1.get(k, 0) - st0.get(k, 0)   # noqa: E731
-    if d("res_rollbacks") or d("tile_rollbacks"):
+    if d("tile_rollbacks"):
         return st1.get("hashed_form", st1.get("form")), False
-    if d("res_steps") == steps:
-        return 6, True
     if d("tile_steps") == steps:
         return 5, True
     return st1.get("hashed_form", st1.get("form")), True
@@ -327,7 +325,7 @@ def traffic_from_profiles(cfg: str, dtype: str, P: int, scaling: str, suffix: st
     """(upper, lower, source) HBM bytes per step-kernel launch from the
     committed PMC summary (profiles/pmc_traffic.json, profiles/collect_pmc.py);
     keyed by config and dtype for one GPU, with a _p<N> suffix for strong
-    shards and _tile / _res when the tile / resident form stepped the timed region.  (None,
+    shards and _tile when the tile form stepped the timed region.  (None, None,
     None, None) when that shape was never collected."""
     rel = os.path.join("profiles", "pmc_traffic.json")
     key = f"{cfg}_{dtype}" if P == 1 or scaling == "weak" else f"{cfg}_{dtype}_p{P}"
@@ -475,10 +473,7 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     form, clean = region_form(st0, st1, args.steps) if P == 1 else (st1.get("hashed_form", st1.get("form")), True)
     traffic, traffic_lower, traffic_src, traffic_same_build = traffic_from_profiles(
-        args.config, args.dtype, P, args.scaling, {5: "_tile", 6: "_res"}.get(form, ""))
-    if form == 6:
-        timing += (f"; the resident form steps a window of {st1.get('res_window')} steps per launch: "
-                   f"avg_launch_ms and algorithmic_bytes_per_launch are per step")
+        args.config, args.dtype, P, args.scaling, "_tile" if form == 5 else "")
     if not clean:
         traffic = traffic_lower = traffic_src = None
         timing += "; MIXED region: a roll-back inside it was replayed by the hashed forms"

@@ -285,13 +285,13 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
  * ABI note: librbhip 0.3 (rb_version) renumbered the counters of 0.2 — the
  * round-4 block counters were removed and RB_STAT_FORM, _BUCKETS,
  * _MAX_PARTNERS and _IO_* moved (8 -> 1, 19 -> 6, 20 -> 7, 27/28 -> 8/9;
- * RB_STATS_COUNT 30 -> 18, then 27 with the resident counters appended).  A
+ * RB_STATS_COUNT 30 -> 18, then 19 with RB_STAT_HASHED_FORM appended).  A
  * consumer built against the 0.2 header must be rebuilt; from 0.3 on new
  * counters are only appended. */
 #define RB_STAT_GRAPHS          0   /* captured step graphs alive               */
 #define RB_STAT_FORM            1   /* step kernel form of the next run: 0 one-lane, 1 cooperative, 2 wide,
                                        3 cooperative + helper, 4 wide + helper (hashed cells),
-                                       5 cell-ordered tiles (rb_tiles.hip), 6 resident windows (rb_resident.hip) */
+                                       5 cell-ordered tiles (rb_tiles.hip) */
 #define RB_STAT_BOX_OPT         2   /* box worlds: chunks replayed without the box kernel */
 #define RB_STAT_BOX_ROLLBACK    3   /* of which rolled back and replayed with it (a body was deferred) */
 #define RB_STAT_REFITS          4   /* broadphase layout refits of a drifting scene (chunk rolled back, replayed) */
@@ -309,19 +309,9 @@ int rb_query(rb_world *w, int64_t *n_owned, int64_t *bytes_per_body_step);
 #define RB_STAT_TILE_SLOTS     15   /* tile slots of the periodic tile grid (workgroups per step) */
 #define RB_STAT_TILE_COLS      16   /* columns per tile edge                    */
 #define RB_STAT_TILE_ON        17   /* the next run of >= 2 steps would use the tile form */
-#define RB_STAT_RES_WINDOWS    18   /* windows stepped in the resident form (one launch each) */
-#define RB_STAT_RES_STEPS      19   /* steps of those windows committed (checked) */
-#define RB_STAT_RES_ROLLBACKS  20   /* resident windows rolled back and replayed by the hashed-cell forms */
-#define RB_STAT_RES_WHY        21   /* why bits of the rolled-back resident windows (OR; 1 slot capacity, 8 partners,
-                                       16 position, 32 candidate list, 64 import table, 128 skin, 256 home-tile
-                                       drift, 512 a neighbour wait timed out) */
-#define RB_STAT_RES_SLOTS      22   /* slots (single-wave workgroups) of the resident tiling */
-#define RB_STAT_RES_ON         23   /* the next run of >= 2 steps would use the resident form */
-#define RB_STAT_RES_WINDOW     24   /* steps per resident window now */
-#define RB_STAT_RES_FITS       25   /* resident tilings fitted */
-#define RB_STAT_HASHED_FORM    26   /* the hashed-cell form (0-4, as RB_STAT_FORM) the world steps with when
-                                       neither the tile nor the resident form does */
-#define RB_STATS_COUNT         27
+#define RB_STAT_HASHED_FORM    18   /* the hashed-cell form (0-4, as RB_STAT_FORM) the world steps with when
+                                       the tile form does not */
+#define RB_STATS_COUNT         19
 int rb_world_stats(rb_world *w, int64_t *out, int32_t n);
 int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches);
 

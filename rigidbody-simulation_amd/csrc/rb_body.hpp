@@ -52,9 +52,9 @@ template <typename T> struct LazyInvI {
 };
 
 // one contact of body i through the reference's skip rules then K2
-template <typename T, typename INV = LazyInvI<T>>
+template <typename T>
 __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Contact<T> &con, V3<T> x, V3<T> n,
-                                              T m, T k, INV &invI, V3<T> &v, V3<T> &w) {
+                                              T m, T k, LazyInvI<T> &invI, V3<T> &v, V3<T> &w) {
     if (!(con.dist < T(0))) return;                 // collision.py:74 (NaN fails too)
     if (absval(con.dist) < p.thr) return;           // collision.py:79-80
     const V3<T> r = {con.pos.x - x.x, con.pos.y - x.y, con.pos.z - x.z};   // :75
@@ -65,8 +65,8 @@ __device__ __forceinline__ void solve_contact(const StepParams<T> &p, const Cont
 
 // a4 (collision.py:66-70): gravity plus the optional applied force / torque
 // (XFRC false: a caller whose worlds never carry one, so no branch on it)
-template <typename T, bool XFRC = true, typename INV = LazyInvI<T>>
-__device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T m, INV &invI, V3<T> &v,
+template <typename T, bool XFRC = true>
+__device__ __forceinline__ void apply_force(const StepParams<T> &p, int32_t l, T m, LazyInvI<T> &invI, V3<T> &v,
                                             V3<T> &w) {
     V3<T> F = {m * p.g[0], m * p.g[1], m * p.g[2]};
     if (XFRC && p.xfrc) F = {p.xfrc[l] + F.x, p.xfrc[p.S + l] + F.y, p.xfrc[2 * p.S + l] + F.z};

@@ -323,42 +323,14 @@ struct rb_world {
     int64_t *tile_pub_host = nullptr, *tile_pub_host_d = nullptr;   // pinned, mapped: why, commits (tile graphs' publish)
     bool tile_pub = false;         // err_pub, and the last graph was a tile run's (tile_pub_host is current)
     unsigned long long tile_commits_seen = 0;
-    // a run of steps whose check waits for the next sync point: a tile run,
-    // or one window of the resident form (res)
-    struct TileRun { int64_t c0, n; double dt, e, mu, thr; bool res; };
+    // a tile run whose check waits for the next sync point
+    struct TileRun { int64_t c0, n; double dt, e, mu, thr; };
     std::vector<TileRun> tile_pending;    // runs enqueued since the last check
     int64_t tile_stats[4] = {};    // runs, steps committed, runs rolled back, bin builds
     int32_t tile_why_seen = 0;     // why bits of the runs rolled back (OR)
     int32_t tile_backoff = 0, tile_skip = 0;   // eligible runs to step hashed after a roll-back (doubling)
     bool tile_replaying = false;   // tile_finish's replay steps hashed
 
-    // the resident form (rb_resident.hip): windows of steps in
-    // one launch each, sphere worlds on one rank.  A window reads the
-    // id-ordered state and commits its end state back only if no slot failed
-    // (its check and roll-back are the tile runs': tile_pending, tile_finish)
-    int res_mode = 0;              // RBHIP_RESIDENT: 0 off (default until measured faster), 1 every eligible world, -1 auto (res_min..res_max bodies)
-    int64_t res_min_bodies = 4097, res_max_bodies = 131072;
-    bool res_fit_valid = false;
-    bool res_declined = false;     // the fit found no tiling (a slot over its capacity, or too many slots)
-    double res_L = 0, res_R = 0, res_ox = 0, res_oy = 0;   // tile side, export band, grid origin
-    int32_t res_ntx = 0, res_nty = 0, res_ncx = 0;
-    double res_fill = 0.7;         // the fit's largest tile occupancy / RES_CAP (RBHIP_RES_FILL)
-    int32_t res_window = 512;      // steps per window (one launch)
-    int32_t res_window_max = 512;  // RBHIP_RES_WINDOW
-    // constants by type (ResParams::types): <= RES_TYPES distinct (m, I, r), else no resident form
-    int32_t res_ntypes = 0;
-    double res_type_val[RES_TYPES][5] = {};
-    uint8_t *res_type_of = nullptr;  // [N]
-    int64_t res_max_slots = 0;     // slots the GPU holds resident at once (with a margin)
-    void *res_mem = nullptr;       // counts, ids, publication, staging
-    size_t res_mem_bytes = 0;
-    uint32_t *res_epoch = nullptr; // [1] tag base of the next window (advanced by the commit kernel)
-    int32_t *res_abort = nullptr;  // [1]
-    uint64_t res_epoch_host = 1;   // the device word's value once the enqueued windows ran
-    int32_t res_backoff = 0, res_skip = 0;   // eligible runs to step otherwise after a roll-back (doubling)
-    int32_t res_fails = 0;         // roll-backs in a row (auto mode retires the form after RES_MAX_FAILS)
-    int64_t res_stats[4] = {};     // windows, steps committed, windows rolled back, fits
-    int32_t res_why_seen = 0;
 
     int sp() const { return (int)(c % 2); }
 };
@@ -1088,10 +1060,9 @@ template <typename T> TileBins<T> tile_bins(const rb_world *w, int sp) {
 // far, folded onto many mostly empty slots, or device memory short): the
 // world steps hashed from now on
 constexpr int TILE_DECLINED = 1;
-constexpr int RES_MAX_FAILS = 6;   // resident roll-backs in a row after which auto mode retires the form
 constexpr size_t TILE_AUTO_MAX_BYTES_PER_BODY = 2048;   // flat scenes need ~0.4 KB
 
-// the words the pending runs' checks read (tile runs and resident windows)
+// the words the pending tile runs' checks read
 int tile_alloc_words(rb_world *w) {
     if (w->tile_gen) return RB_OK;
     HIPCHK(hipMalloc((void **)&w->tile_gen, 2 * sizeof(uint32_t)));
@@ -1244,7 +1215,7 @@ int tile_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr)
     }
     w->tile_valid_sp = w->sp();
     w->primed = false;                               // the hashed forms' table is stale
-    w->tile_pending.push_back(rb_world::TileRun{c0, n, dt, e, mu, thr, false});
+    w->tile_pending.push_back(rb_world::TileRun{c0, n, dt, e, mu, thr});
     w->tile_stats[0] += 1;
     return RB_OK;
 }
@@ -1276,16 +1247,7 @@ int tile_finish(rb_world *w) {
     w->tile_commits_seen = commits;
     std::vector<rb_world::TileRun> runs;
     runs.swap(w->tile_pending);
-    bool res_ok = false;
-    for (size_t k = 0; k < ok && k < runs.size(); ++k) {
-        (runs[k].res ? w->res_stats[1] : w->tile_stats[1]) += runs[k].n;
-        res_ok |= runs[k].res;
-    }
-    if (res_ok) {
-        // committed windows: the form works on this scene (grow the window back)
-        w->res_fails = 0;
-        if (w->res_backoff > 0) w->res_backoff /= 2;
-    }
+    for (size_t k = 0; k < ok && k < runs.size(); ++k) w->tile_stats[1] += runs[k].n;
     if (!(err & ERR_TILE)) {
         if (w->tile_backoff > 0) w->tile_backoff /= 2;
         return RB_OK;
@@ -1295,7 +1257,6 @@ int tile_finish(rb_world *w) {
     // replay grows max_partners or refits the table as a synchronous
     // rb_step would)
     const size_t first = std::min(ok, runs.size());
-    const bool res_failed = first < runs.size() && runs[first].res;
     const int32_t clean = err & ~ERR_TILE;
     w->err_pub = false;
     HIPCHK(hipMemcpyAsync(w->err, &clean, sizeof(int32_t), hipMemcpyHostToDevice, w->stream));
@@ -1303,29 +1264,14 @@ int tile_finish(rb_world *w) {
     HIPCHK(hipStreamSynchronize(w->stream));
     w->tile_valid_sp = -1;
     w->primed = false;
-    if (res_failed) {
-        // a resident window: a body outran the skin (or its home tile) —
-        // shorter windows; a slot, list or import table overflowed — a new
-        // fit; then back off before the next try.  Auto mode retires the
-        // form after RES_MAX_FAILS roll-backs in a row.
-        w->res_stats[2] += 1;
-        w->res_why_seen |= why;
-        // a body left the grid, or a slot / publication / import table
-        // overflowed: a new fit from the positions the replay reaches
-        if (why & (RES_WHY_GRID | TILE_WHY_CAP | RES_WHY_IMPORT | RES_WHY_PUB)) w->res_fit_valid = false;
-        w->res_backoff = w->res_backoff ? std::min(2 * w->res_backoff, 64) : 1;
-        w->res_skip = w->res_backoff;
-        if (++w->res_fails >= RES_MAX_FAILS && w->res_mode == -1) w->res_mode = 0;
-    } else {
-        w->tile_stats[2] += 1;
-        w->tile_why_seen |= why;
-        if (why & (TILE_WHY_CAP | TILE_WHY_WINDOW)) w->tile_fit_valid = false;   // the scene outgrew the fit
-        w->tile_backoff = w->tile_backoff ? std::min(2 * w->tile_backoff, 64) : 1;
-        w->tile_skip = w->tile_backoff;
-        // auto mode: a scene that outgrew the tile slots once (pile-ups) tends to
-        // keep doing so, and every retry costs a roll-back — step hashed from now on
-        if (w->tile_mode == -1) w->tile_mode = 0;
-    }
+    w->tile_stats[2] += 1;
+    w->tile_why_seen |= why;
+    if (why & (TILE_WHY_CAP | TILE_WHY_WINDOW)) w->tile_fit_valid = false;   // the scene outgrew the fit
+    w->tile_backoff = w->tile_backoff ? std::min(2 * w->tile_backoff, 64) : 1;
+    w->tile_skip = w->tile_backoff;
+    // auto mode: a scene that outgrew the tile slots once (pile-ups) tends to
+    // keep doing so, and every retry costs a roll-back — step hashed from now on
+    if (w->tile_mode == -1) w->tile_mode = 0;
     w->c = first < runs.size() ? runs[first].c0 : w->c;
     const bool saved = w->sync_call;
     w->sync_call = true;
@@ -1340,273 +1286,6 @@ int tile_finish(rb_world *w) {
     return rc;
 }
 
-// ---- the resident form (rb_resident.hip) ------------------------
-bool res_eligible(const rb_world *w) {
-    if (w->res_mode == 0 || w->res_declined || w->tile_replaying || w->P != 1 || !w->all_spheres ||
-        w->law != RB_LAW_MUJOCO || w->xfrc || w->timing)
-        return false;
-    if (w->maxp > 32 || w->n_local <= 0 || w->N >= (int64_t)1 << RES_ID_BITS || w->res_ntypes < 1) return false;
-    return w->res_mode == 1 || (w->n_local >= w->res_min_bodies && w->n_local <= w->res_max_bodies);
-}
-
-// slots of one world's grid the GPU holds resident at once, with a margin
-// (workgroups are dealt round-robin over the XCDs, empty slots included)
-int64_t res_capacity(rb_world *w) {
-    if (w->res_max_slots > 0) return w->res_max_slots;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, w->device) != hipSuccess) cus = 0;
-    const int per_cu = res_blocks_per_cu(w->dtype == RB_F64, w->maxp);
-    w->res_max_slots = (int64_t)cus * per_cu * 7 / 8;
-    return w->res_max_slots;
-}
-
-// The tiling from body positions (x, y at pos[k * stride], pos[k * stride + 1]):
-// the export band R = the largest contact reach (2 rmax, with a margin), the
-// search cell 2 R; the largest tile side L in [3 R, (RES_CELLS^1/2 - 1) 2 R - 2 R]
-// whose fullest tile holds at most res_fill x RES_CAP bodies (room for the
-// bodies that move in before the next fit); the grid covers the scene's
-// extent plus a ring of one tile.  A scene no tiling fits (a tile over that
-// occupancy at the smallest side, or more slots than the GPU holds resident)
-// is declined until its next rb_set_state.
-void res_fit(rb_world *w, const double *pos, int64_t stride) {
-    w->res_stats[3] += 1;
-    w->res_fit_valid = true;
-    w->res_declined = false;
-    const double R = 2.0 * w->rmax * (1.0 + 1e-6) + 1e-12;
-    const double cs = 2.0 * R * (1.0 + 1e-6);
-    std::vector<double> xs, ys;
-    xs.reserve((size_t)w->N);
-    ys.reserve((size_t)w->N);
-    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
-    for (int64_t b = 0; b < w->N; ++b) {
-        const double x = pos[b * stride], y = pos[b * stride + 1];
-        if (!(fabs(x) < 1e9 && fabs(y) < 1e9)) { w->res_declined = true; return; }
-        xs.push_back(x);
-        ys.push_back(y);
-        lo[0] = std::min(lo[0], x); hi[0] = std::max(hi[0], x);
-        lo[1] = std::min(lo[1], y); hi[1] = std::max(hi[1], y);
-    }
-    if (xs.empty()) { w->res_declined = true; return; }
-    const int64_t limit = std::max<int64_t>(1, (int64_t)(w->res_fill * RES_CAP));
-    std::vector<int64_t> t(xs.size());
-    auto worst = [&](double L) {
-        const double inv = 1.0 / L;
-        for (size_t k = 0; k < xs.size(); ++k)
-            t[k] = (((int64_t)floor((xs[k] - lo[0]) * inv)) << 31) | (int64_t)floor((ys[k] - lo[1]) * inv);
-        std::sort(t.begin(), t.end());
-        int64_t m = 0;
-        for (size_t a = 0; a < t.size();) {
-            size_t e = a;
-            while (e < t.size() && t[e] == t[a]) ++e;
-            m = std::max<int64_t>(m, (int64_t)(e - a));
-            a = e;
-        }
-        return m;
-    };
-    const int side = (int)floor(sqrt((double)RES_CELLS));
-    const double Lmin = 3.0 * R, Lmax = (side - 1) * cs - 2.0 * R;
-    if (Lmax < Lmin || worst(Lmin) > limit) { w->res_declined = true; return; }
-    double L = Lmin;
-    while (L * 1.25 <= Lmax && worst(L * 1.25) <= limit) L *= 1.25;
-    for (int k = 0; k < 6; ++k) {                    // (bisect the last factor)
-        const double mid = L * (1.0 + 0.25 / (2 << k));
-        if (mid <= Lmax && worst(mid) <= limit) L = mid;
-    }
-    // the grid: the extent's tiles plus a ring of one (origin on a multiple of L)
-    const double ox = (floor(lo[0] / L) - 1.0) * L, oy = (floor(lo[1] / L) - 1.0) * L;
-    const int64_t ntx = (int64_t)floor((hi[0] - ox) / L) + 2, nty = (int64_t)floor((hi[1] - oy) / L) + 2;
-    if (ntx * nty > res_capacity(w) || ntx * nty > INT32_MAX / (8 * RES_CAP)) { w->res_declined = true; return; }
-    w->res_L = L;
-    w->res_R = R;
-    w->res_ox = ox;
-    w->res_oy = oy;
-    w->res_ntx = (int32_t)ntx;
-    w->res_nty = (int32_t)nty;
-    w->res_ncx = (int32_t)ceil((L + 2.0 * R) / cs) + 1;
-    if (w->res_ncx * w->res_ncx > RES_CELLS) { w->res_declined = true; return; }
-}
-
-size_t res_bytes(const rb_world *w, size_t *o_ids, size_t *o_pub, size_t *o_snap, size_t *o_st) {
-    const size_t slots = (size_t)w->res_ntx * w->res_nty, esz = (size_t)w->esz;
-    auto up = [](size_t v) { return (v + 255) / 256 * 256; };
-    size_t o = up(slots * 4);
-    *o_ids = o;
-    o += up(slots * RES_CAP * 4);
-    *o_pub = o;
-    o += up(2 * slots * RES_PUB_WORDS * 8);
-    *o_snap = o;
-    o += up((size_t)w->Npad * 4 * esz);
-    *o_st = o;
-    o += up((size_t)10 * w->S * esz);
-    return o;
-}
-
-int res_alloc(rb_world *w) {
-    size_t oi, op, os, ot;
-    const size_t need = res_bytes(w, &oi, &op, &os, &ot);
-    if (w->res_mem && w->res_mem_bytes >= need) return RB_OK;
-    HIPCHK(hipStreamSynchronize(w->stream));
-    drop_graphs(w);                                  // captured buffer pointers
-    if (w->res_mem) { HIPCHK(hipFree(w->res_mem)); w->res_mem = nullptr; w->res_mem_bytes = 0; }
-    if (hipMalloc(&w->res_mem, need) != hipSuccess) {
-        (void)hipGetLastError();
-        w->res_mem = nullptr;
-        if (w->res_mode == -1) { w->res_mode = 0; return TILE_DECLINED; }
-        return fail(RB_ENOMEM, "resident form: hipMalloc of %zu bytes failed", need);
-    }
-    w->res_mem_bytes = need;
-    // granule tags 0: older than every window's (res_epoch starts at 1)
-    HIPCHK(hipMemsetAsync(w->res_mem, 0, need, w->stream));
-    if (!w->res_epoch) {
-        HIPCHK(hipMalloc((void **)&w->res_epoch, 256));
-        w->res_abort = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(w->res_epoch) + 128);
-    }
-    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w->res_epoch, 1, 1, w->stream));
-    HIPCHK(hipMemsetAsync(w->res_abort, 0, sizeof(int32_t), w->stream));
-    w->res_epoch_host = 1;
-    if (int rc = tile_alloc_words(w)) return rc;
-    return RB_OK;
-}
-
-template <typename T> ResParams<T> make_res(rb_world *w, int64_t c0, int32_t K, bool rec, double dt, double e, double mu,
-                                            double thr) {
-    size_t oi, op, os, ot;
-    res_bytes(w, &oi, &op, &os, &ot);
-    char *m = static_cast<char *>(w->res_mem);
-    ResParams<T> p{};
-    p.sp = make_step<T>(w, c0, dt, e, mu, thr, false);   // (err_pub cleared)
-    if (!rec) {
-        p.sp.rec_count = nullptr;
-        p.sp.rec_partner = nullptr;
-        p.sp.rec_kind = nullptr;
-        p.sp.rec_dist = nullptr;
-    }
-    p.cnt = reinterpret_cast<const int32_t *>(m);
-    p.ids = reinterpret_cast<const int32_t *>(m + oi);
-    p.snap = dp<Snap<T>>(w->snap[c0 % 2], 0);
-    p.pub = reinterpret_cast<unsigned long long *>(m + op);
-    p.out_snap = reinterpret_cast<Snap<T> *>(m + os);
-    p.out_st = reinterpret_cast<T *>(m + ot);
-    p.epoch = w->res_epoch;
-    p.abort = w->res_abort;
-    p.why = w->tile_why;
-    p.ntx = w->res_ntx;
-    p.nty = w->res_nty;
-    p.K = K;
-    p.ox = (T)w->res_ox;
-    p.oy = (T)w->res_oy;
-    p.L = (T)w->res_L;
-    p.inv_L = (T)(1.0 / w->res_L);
-    p.R = (T)w->res_R;
-    p.inv_cs = (T)(1.0 / (2.0 * w->res_R * (1.0 + 1e-6)));
-    p.ncx = w->res_ncx;
-    p.type_of = w->res_type_of;
-    for (int t = 0; t < RES_TYPES; ++t)
-        for (int k = 0; k < 5; ++k) p.types[t][k] = (T)w->res_type_val[t][k];
-    p.rec = rec ? 1 : 0;
-    p.timeout = 5000000;                             // 50 ms of s_memrealtime (100 MHz)
-    return p;
-}
-
-template <typename T> ResCommit<T> make_res_commit(rb_world *w, int64_t c_end, int32_t K) {
-    size_t oi, op, os, ot;
-    res_bytes(w, &oi, &op, &os, &ot);
-    char *m = static_cast<char *>(w->res_mem);
-    ResCommit<T> p{};
-    p.err = w->err;
-    p.out_snap = reinterpret_cast<const Snap<T> *>(m + os);
-    p.out_st = reinterpret_cast<const T *>(m + ot);
-    p.snap = dp<Snap<T>>(w->snap[c_end % 2], 0);
-    p.st = BodyState<T>{dp<T>(w->state, 0), w->S};
-    p.n = w->N;
-    p.S = w->S;
-    p.epoch = w->res_epoch;
-    p.K = K;
-    p.abort = w->res_abort;
-    p.commits = w->tile_commits;
-    return p;
-}
-
-// One run of n steps in windows of res_window steps from step c, graph-
-// replayed (per window: clear the slot counts, bin, the resident kernel, the
-// commit), each window recorded as pending until checked.
-int res_run(rb_world *w, int64_t n, double dt, double e, double mu, double thr) {
-    if (!w->res_fit_valid) {
-        if (int rc = finish_pending(w)) return rc;   // (the fit reads the id-ordered state)
-        if (w->io_q_h && w->mirror_version == w->state_version) {
-            res_fit(w, w->io_q_h, 7);
-        } else {
-            std::vector<double> q((size_t)4 * w->N);
-            if (w->dtype == RB_F64) {
-                HIPCHK(hipMemcpyAsync(q.data(), w->snap[w->sp()], sizeof(double) * q.size(), hipMemcpyDeviceToHost, w->stream));
-                HIPCHK(hipStreamSynchronize(w->stream));
-            } else {
-                std::vector<float> f(q.size());
-                HIPCHK(hipMemcpyAsync(f.data(), w->snap[w->sp()], sizeof(float) * f.size(), hipMemcpyDeviceToHost, w->stream));
-                HIPCHK(hipStreamSynchronize(w->stream));
-                for (size_t k = 0; k < f.size(); ++k) q[k] = f[k];
-            }
-            res_fit(w, q.data(), 4);
-        }
-        drop_graphs(w);                              // the tiling is a captured kernel argument
-        if (w->res_declined) return TILE_DECLINED;
-    }
-    if (int rc = res_alloc(w)) return rc;
-    const bool f64 = w->dtype == RB_F64;
-    const int32_t Kw = std::max(2, w->res_window);
-    // tags are 32-bit: restart them (granules zeroed) well before they wrap
-    if (w->res_epoch_host + (uint64_t)n + (uint64_t)(n / Kw + 2) * 2 > 0xf0000000ull) {
-        HIPCHK(hipStreamSynchronize(w->stream));
-        size_t oi, op, os, ot;
-        res_bytes(w, &oi, &op, &os, &ot);
-        HIPCHK(hipMemsetAsync(static_cast<char *>(w->res_mem) + op, 0, os - op, w->stream));
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w->res_epoch, 1, 1, w->stream));
-        w->res_epoch_host = 1;
-    }
-    const size_t slots = (size_t)w->res_ntx * w->res_nty;
-    // graphs of at most 16 windows (a long run replays several)
-    const int64_t chunk = 16 * (int64_t)Kw;
-    if (n > chunk) {
-        for (int64_t left = n; left > 0;) {
-            const int64_t nn = std::min(left, chunk);
-            const bool saved = w->record;
-            w->record = saved && nn == left;         // (only the run's last step is recorded)
-            const int rc = res_run(w, nn, dt, e, mu, thr);
-            w->record = saved;
-            if (rc) return rc;
-            left -= nn;
-        }
-        return RB_OK;
-    }
-    const int64_t c0 = w->c;
-    const int variant = 16 | 64 | (int)w->record | (Kw << 8);
-    int rc = graph_replay(w, n, variant, dt, e, mu, thr, [&](hipStream_t s, int64_t cs) {
-        for (int64_t k0 = 0; k0 < n; k0 += Kw) {
-            const int32_t K = (int32_t)std::min<int64_t>(Kw, n - k0);
-            const bool rec = w->record && k0 + K == n;
-            HIPCHK(hipMemsetAsync(w->res_mem, 0, slots * 4, s));
-            HIPCHK(f64 ? launch_res_bin<double>(make_res<double>(w, cs + k0, K, rec, dt, e, mu, thr), w->N, s)
-                       : launch_res_bin<float>(make_res<float>(w, cs + k0, K, rec, dt, e, mu, thr), w->N, s));
-            HIPCHK(f64 ? launch_res_step<double>(make_res<double>(w, cs + k0, K, rec, dt, e, mu, thr), w->maxp, s)
-                       : launch_res_step<float>(make_res<float>(w, cs + k0, K, rec, dt, e, mu, thr), w->maxp, s));
-            HIPCHK(f64 ? launch_res_commit<double>(make_res_commit<double>(w, cs + k0 + K, K), s)
-                       : launch_res_commit<float>(make_res_commit<float>(w, cs + k0 + K, K), s));
-        }
-        return (int)RB_OK;
-    });
-    if (rc) return rc;
-    for (int64_t k0 = 0; k0 < n; k0 += Kw) {
-        const int64_t K = std::min<int64_t>(Kw, n - k0);
-        w->tile_pending.push_back(rb_world::TileRun{c0 + k0, K, dt, e, mu, thr, true});
-        w->res_epoch_host += (uint64_t)K + 1;
-        w->res_stats[0] += 1;
-    }
-    w->c += n;
-    w->tile_valid_sp = -1;                           // (the tile bins, if any, are stale)
-    w->primed = false;                               // the hashed forms' table is stale
-    return RB_OK;
-}
-
 // nsteps steps (sharded: with the in-library exchange), graph-replayed
 int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, double thr, bool sharded) {
     if (nsteps < 0) return fail(RB_EINVAL, "nsteps < 0");
@@ -1617,15 +1296,6 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         return fail(RB_EINVAL, "invalid step parameters dt=%g e=%g mu=%g thr=%g", dt, e, mu, thr);
     if (nsteps == 0) return RB_OK;
     HIPCHK(hipSetDevice(w->device));
-    // the resident form for runs of >= 2 steps (windows chain like tile runs)
-    const bool res = !sharded && res_eligible(w) && nsteps >= 2 && w->tile_pending.size() < 256;
-    if (res && w->res_skip > 0) {
-        --w->res_skip;                               // (back-off after a roll-back: this run steps otherwise)
-    } else if (res) {
-        w->state_version += 1;
-        const int rc = res_run(w, nsteps, dt, e, mu, thr);
-        if (rc != TILE_DECLINED) return rc;          // (declined: the forms below)
-    }
     // the tile form for runs of >= 2 steps, or to continue from its bins;
     // pending tile runs chain (their check waits for the next sync point),
     // anything else first settles them
@@ -1923,27 +1593,6 @@ int upload_consts(rb_world *w, const rb_scene_desc *d, std::vector<double> &boun
             w->tile_ntypes = (int32_t)types.size();
         }
     }
-    // the resident form's constant types: distinct (m, ix, iy, iz, r) as the
-    // arithmetic type holds them (a migrant or export carries its type)
-    {
-        std::vector<std::array<T, 5>> types;
-        std::vector<uint8_t> type_of((size_t)w->N, 0);
-        for (int64_t b = 0; b < w->N && types.size() <= (size_t)RES_TYPES; ++b) {
-            const std::array<T, 5> t = {(T)d->mass[b], (T)d->inertia[3 * b], (T)d->inertia[3 * b + 1],
-                                        (T)d->inertia[3 * b + 2], (T)bound[(size_t)b]};
-            size_t k = 0;
-            while (k < types.size() && memcmp(types[k].data(), t.data(), sizeof(t)) != 0) ++k;
-            if (k == types.size()) types.push_back(t);
-            type_of[(size_t)b] = (uint8_t)k;
-        }
-        if (types.size() <= (size_t)RES_TYPES) {
-            for (size_t t = 0; t < types.size(); ++t)
-                for (int k = 0; k < 5; ++k) w->res_type_val[t][k] = (double)types[t][k];
-            HIPCHK(hipMalloc((void **)&w->res_type_of, (size_t)w->N));
-            WCHK(wput(w, w->res_type_of, type_of.data(), (size_t)w->N));
-            w->res_ntypes = (int32_t)types.size();
-        }
-    }
     std::vector<int32_t> k((size_t)w->Npad, 0);
     for (int64_t b = 0; b < w->N; ++b) k[(size_t)b] = d->kind[b];
     WCHK(wput(w, w->kind, k.data(), sizeof(int32_t) * k.size()));
@@ -1961,8 +1610,7 @@ void free_world(rb_world *w) {
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     if (w->opt_save) (void)hipFree(w->opt_save);
-    void *tbufs[] = {w->tile_mem, w->tile_fill, w->tile_gen, w->tile_why, w->tile_commits, w->tile_type_of,
-                     w->res_mem, w->res_epoch, w->res_type_of};
+    void *tbufs[] = {w->tile_mem, w->tile_fill, w->tile_gen, w->tile_why, w->tile_commits, w->tile_type_of};
     for (void *b : tbufs)
         if (b) (void)hipFree(b);
     if (w->tile_host) (void)hipHostFree(w->tile_host);
@@ -2057,14 +1705,6 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // from 73,984 up
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
     if (const char *ev = getenv("RBHIP_TILE_MIN_BODIES")) w->tile_min_bodies = atoll(ev);
-    // the resident form (rb_resident.hip): RBHIP_RESIDENT = 0 off, 1 every
-    // eligible world, -1 auto (RBHIP_RES_MIN_BODIES .. RBHIP_RES_MAX_BODIES
-    // bodies, retired after RES_MAX_FAILS roll-backs in a row)
-    if (const char *ev = getenv("RBHIP_RESIDENT")) w->res_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
-    if (const char *ev = getenv("RBHIP_RES_MIN_BODIES")) w->res_min_bodies = atoll(ev);
-    if (const char *ev = getenv("RBHIP_RES_MAX_BODIES")) w->res_max_bodies = atoll(ev);
-    if (const char *ev = getenv("RBHIP_RES_WINDOW")) w->res_window = w->res_window_max = std::max(2, std::min(4096, atoi(ev)));
-    if (const char *ev = getenv("RBHIP_RES_FILL")) w->res_fill = std::max(0.1, std::min(1.0, atof(ev)));
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
     // buckets: cooperative worlds (a hash per cell; they also keep a slot
@@ -2328,8 +1968,6 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     w->primed = false;
     w->tile_valid_sp = -1;
     w->tile_fit_valid = false;                           // (refitted at the next tile run)
-    w->res_fit_valid = false;                            // (and resident run)
-    w->res_declined = false;
     w->state_version += 1;
     // uploading the staging's bytes yields exactly this state (one rank)
     w->mirror_version = w->P == 1 ? w->state_version : -1;
@@ -2805,17 +2443,13 @@ int rb_world_stats(rb_world *w, int64_t *out, int32_t n) {
     if (!w || (n > 0 && !out)) return fail(RB_EINVAL, "null argument");
     HIPCHK(hipSetDevice(w->device));
     if (int rc = finish_pending(w)) return rc;
-    const bool res = res_eligible(w);
     const bool tile = tile_eligible(w);
-    const int form = res && w->res_skip == 0 ? FORM_RESIDENT : tile ? FORM_TILE : step_form(w);
+    const int form = tile ? FORM_TILE : step_form(w);
     const int64_t v[RB_STATS_COUNT] = {(int64_t)w->graphs.size(), form, w->box_stats[0], w->box_stats[1], w->refits,
                                        w->table_grows, w->H, (int64_t)w->maxp, w->io_stats[0], w->io_stats[1],
                                        w->tile_stats[0], w->tile_stats[1], w->tile_stats[2], w->tile_stats[3],
                                        (int64_t)w->tile_why_seen, (int64_t)w->tile_ntx * w->tile_nty,
-                                       (int64_t)w->tile_tc, tile && w->tile_skip == 0 ? 1 : 0,
-                                       w->res_stats[0], w->res_stats[1], w->res_stats[2], (int64_t)w->res_why_seen,
-                                       (int64_t)w->res_ntx * w->res_nty, res && w->res_skip == 0 ? 1 : 0,
-                                       (int64_t)w->res_window, w->res_stats[3], step_form(w)};
+                                       (int64_t)w->tile_tc, tile && w->tile_skip == 0 ? 1 : 0, step_form(w)};
     for (int32_t k = 0; k < n && k < RB_STATS_COUNT; ++k) out[k] = v[k];
     return n < RB_STATS_COUNT ? n : RB_STATS_COUNT;
 }

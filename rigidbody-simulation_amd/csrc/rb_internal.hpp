@@ -345,83 +345,10 @@ template <typename T> hipError_t launch_tile_step(const TileParams<T> &p, int ma
 template <typename T> hipError_t launch_tile_build(const TileIO<T> &p, hipStream_t s);   // bins zeroed by the caller
 template <typename T> hipError_t launch_tile_unbin(const TileIO<T> &p, hipStream_t s);
 
-// ---- the resident form (rb_resident.hip) ---------------------------
-// Sphere worlds on one rank.  One launch steps a WINDOW of K reference steps.
-// The plane (x, y) over the scene is cut into an ntx x nty grid of square
-// tiles of side L (origin ox, oy; not periodic); one single-wave workgroup
-// per tile ("slot") owns the bodies inside its tile and keeps their state in
-// registers for the whole window.  Each step every slot
-//   - imports from its 8 neighbours the positions of their bodies within the
-//     contact reach R of its tile ("exports") and the full state of bodies
-//     that moved into its tile ("migrants"),
-//   - searches its own bodies' partners among its own bodies and the imports
-//     (LDS cells of side >= 2 R: the 2 x 2 nearest cells hold every partner),
-//     solves and integrates them exactly as the hashed forms do (rb_body.hpp),
-//   - publishes for the next step the exports and migrants of its bodies.
-// The publication is 8-byte {tag = step, 32-bit half} granules stored
-// write-through (sc1), so every word carries its own freshness: a slot waits
-// only for its neighbours, never for the grid.  The end state goes to a
-// staging copy that the commit kernel writes into the id-ordered state only
-// if no slot failed; any failure (a body leaving the grid or moving more
-// than a tile, a full slot or publication, a partner overflow, a bad
-// position, a wait that timed out) raises ERR_TILE with a RES_WHY_* bit and
-// the host replays the window with the hashed forms (rb_capi.hip tile_finish).
-constexpr int RES_CAP = 64;              // bodies per slot: one wave
-constexpr int RES_NIMP = 64;             // imported positions per slot and step (exports in + own emigrants)
-constexpr int RES_EXP_CAP = 32;          // exports per direction and step
-constexpr int RES_MIG_CAP = 8;           // migrants per direction and step
-constexpr int RES_CELLS = 256;           // LDS search cells per slot (the fit keeps (L + 2 R) / 2 R <= 16)
-constexpr int RES_TYPES = 4;             // distinct body constants a resident world may have
-constexpr int RES_ID_BITS = 26;          // an id granule: id | type << RES_ID_BITS
-enum : int32_t { RES_WHY_GRID = 32, RES_WHY_PUB = 64, RES_WHY_IMPORT = 128, RES_WHY_MOVE = 256, RES_WHY_TIMEOUT = 512 };
-template <typename T> struct ResParams {
-    const int32_t *cnt;                  // [slots] bodies binned into each slot at the window start
-    const int32_t *ids;                  // [slots][RES_CAP] their ids (bin order)
-    const Snap<T> *snap;                 // the window-start snapshot (id order; state rows and constants: sp)
-    unsigned long long *pub;             // [2][slots][RES_PUB_WORDS] granules (rb_resident.hip layout)
-    Snap<T> *out_snap;                   // [N] the window-end snapshot (staging, id order)
-    T *out_st;                           // [10][S] the window-end q, v, w (staging)
-    StepParams<T> sp;                    // physics, error word, recording (rb_body.hpp)
-    const uint32_t *epoch;               // tag base of this window (the commit kernel advances it)
-    int32_t *abort;                      // set with any failure: spinning workgroups leave
-    int32_t *why;
-    int32_t ntx, nty, K;                 // tile grid, steps
-    T ox, oy, L, inv_L;                  // grid origin, tile side
-    T R;                                 // export band: the largest contact reach (2 rmax), with a margin
-    T inv_cs;                            // 1 / search cell side (>= 2 R)
-    int32_t ncx;                         // search cells per axis of a slot's window (tile + R each side)
-    // constants by type: worlds whose bodies share at most RES_TYPES distinct
-    // (m, ix, iy, iz, r) (a migrant or export carries its type with its id)
-    const uint8_t *type_of;              // [N]
-    T types[RES_TYPES][5];
-    int32_t rec;                         // record the window's last step
-    int64_t timeout;                     // s_memrealtime ticks (100 MHz) a wait may spin
-};
-template <typename T> struct ResCommit {
-    const int32_t *err;
-    const Snap<T> *out_snap;
-    const T *out_st;
-    Snap<T> *snap;                       // the id-ordered snapshot of the window-end step parity
-    BodyState<T> st;
-    int64_t n, S;
-    uint32_t *epoch;                     // += K + 1 (the next window's tags lie above this one's)
-    int32_t K;
-    int32_t *abort;                      // cleared
-    unsigned long long *commits;         // += 1 when the window committed
-};
-// granules per slot and parity of the publication (both dtypes)
-constexpr int64_t RES_PUB_WORDS = 6144;
-template <typename T> hipError_t launch_res_bin(const ResParams<T> &p, int64_t n, hipStream_t s);   // cnt zeroed by the caller
-template <typename T> hipError_t launch_res_step(const ResParams<T> &p, int maxp, hipStream_t s);
-template <typename T> hipError_t launch_res_commit(const ResCommit<T> &p, hipStream_t s);
-// workgroups of the resident kernel one CU holds (its LDS and registers)
-int res_blocks_per_cu(int dtype_f64, int maxp);
-
 // launchers (rb_kernels.hip)
 // step kernel forms: one lane per body, 8 lanes per body (small scenes), one
 // lane per body at one wave per SIMD (mid-size scenes)
-enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4, FORM_TILE = 5,
-             FORM_RESIDENT = 6 };
+enum : int { FORM_ONE = 0, FORM_COOP = 1, FORM_WIDE = 2, FORM_COOP_HELP = 3, FORM_WIDE_HELP = 4, FORM_TILE = 5 };
 // boxes: the box-capable instantiation (box-box / sphere-box narrowphase)
 template <typename T> hipError_t launch_step(const StepParams<T> &p, int maxp, int form, bool boxes, hipStream_t s);
 // the wide form's kernel alone (its own translation unit: scheduled for memory clauses)

@@ -81,11 +81,9 @@ SIGNATURES = {
 # rb_world_stats indices (include/rbhip.h RB_STAT_*)
 STAT_NAMES = ["graphs", "form", "box_opt_chunks", "box_rollbacks", "refits", "table_grows", "buckets",
               "max_partners", "io_skipped", "io_uploads", "tile_runs", "tile_steps", "tile_rollbacks",
-              "tile_builds", "tile_why", "tile_slots", "tile_cols", "tile_on", "res_windows", "res_steps",
-              "res_rollbacks", "res_why", "res_slots", "res_on", "res_window", "res_fits", "hashed_form"]
+              "tile_builds", "tile_why", "tile_slots", "tile_cols", "tile_on", "hashed_form"]
 FORM_NAMES = {0: "rb::step_kernel_one", 1: "rb::step_kernel_coop", 2: "rb::step_kernel_wide",
-              3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help", 5: "rb::tile_step_kernel",
-              6: "rb::res_step_kernel"}
+              3: "rb::step_kernel_coop_help", 4: "rb::step_kernel_wide_help", 5: "rb::tile_step_kernel"}
 
 _lib = None
 
