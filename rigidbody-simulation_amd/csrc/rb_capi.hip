@@ -306,6 +306,7 @@ struct rb_world {
     // failed run, which the host replays with the hashed-cell forms
     // (tile_finish) at the next sync point.
     int tile_mode = -1;            // RBHIP_TILE: 0 off, 1 every eligible world, -1 auto (default: >= tile_min_bodies, off after a roll-back)
+    int tile_mode_init = -1;       // the mode at creation (auto: re-armed by an rb_set_state that uploads)
     int32_t tile_ntypes = 0;       // distinct (m, I) of the bodies when <= TILE_TYPES (else 0: no tile form)
     double tile_type_val[TILE_TYPES][4] = {};   // m ix iy iz of each type
     uint8_t *tile_type_of = nullptr;   // [N]
@@ -1077,6 +1078,23 @@ int tile_alloc_words(rb_world *w) {
     return RB_OK;
 }
 
+// Auto mode retires the tile form (a roll-back, or bins it will not
+// allocate): the bins go too (hundreds of MB at millions of bodies), and the
+// graphs that captured their pointers
+int tile_retire(rb_world *w) {
+    w->tile_mode = 0;
+    w->tile_valid_sp = -1;
+    if (!w->tile_mem && !w->tile_fill) return RB_OK;
+    HIPCHK(hipStreamSynchronize(w->stream));
+    drop_graphs(w);
+    if (w->tile_mem) HIPCHK(hipFree(w->tile_mem));
+    if (w->tile_fill) HIPCHK(hipFree(w->tile_fill));
+    w->tile_mem = nullptr;
+    w->tile_fill = nullptr;
+    w->tile_mem_bytes = 0;
+    return RB_OK;
+}
+
 int tile_alloc(rb_world *w) {
     const size_t need = 2 * tile_bins_bytes(w);
     const size_t slots = (size_t)w->tile_ntx * w->tile_nty;
@@ -1085,7 +1103,7 @@ int tile_alloc(rb_world *w) {
         return RB_OK;
     }
     if (w->tile_mode == -1 && need > TILE_AUTO_MAX_BYTES_PER_BODY * (size_t)w->N) {
-        w->tile_mode = 0;
+        if (int rc = tile_retire(w)) return rc;
         return TILE_DECLINED;
     }
     HIPCHK(hipStreamSynchronize(w->stream));
@@ -1099,7 +1117,7 @@ int tile_alloc(rb_world *w) {
         w->tile_mem = nullptr;
         w->tile_mem_bytes = 0;
         if (w->tile_mode == -1) {
-            w->tile_mode = 0;
+            if (int rc = tile_retire(w)) return rc;
             return TILE_DECLINED;
         }
         return fail(RB_ENOMEM, "tile bins: hipMalloc of %zu bytes failed", need);
@@ -1271,7 +1289,8 @@ int tile_finish(rb_world *w) {
     w->tile_skip = w->tile_backoff;
     // auto mode: a scene that outgrew the tile slots once (pile-ups) tends to
     // keep doing so, and every retry costs a roll-back — step hashed from now on
-    if (w->tile_mode == -1) w->tile_mode = 0;
+    if (w->tile_mode == -1)
+        if (int rc = tile_retire(w)) return rc;
     w->c = first < runs.size() ? runs[first].c0 : w->c;
     const bool saved = w->sync_call;
     w->sync_call = true;
@@ -1704,6 +1723,7 @@ int rb_world_create(rb_world **out, const rb_scene_desc *d) {
     // slower than the hashed forms up to 65,536 flat spheres (C3) and faster
     // from 73,984 up
     if (const char *ev = getenv("RBHIP_TILE")) w->tile_mode = atoi(ev) < 0 ? -1 : atoi(ev) ? 1 : 0;
+    w->tile_mode_init = w->tile_mode;
     if (const char *ev = getenv("RBHIP_TILE_MIN_BODIES")) w->tile_min_bodies = atoll(ev);
     if (const char *ev = getenv("RBHIP_BOX_OPTIMISTIC")) w->box_opt = atoi(ev) != 0;
     if (const char *ev = getenv("RBHIP_DIAG_OVERFLOW")) w->diag_overflow = atoi(ev);
@@ -1968,6 +1988,10 @@ int rb_set_state(rb_world *w, const double *qpos, const double *qvel) {
     w->primed = false;
     w->tile_valid_sp = -1;
     w->tile_fit_valid = false;                           // (refitted at the next tile run)
+    if (w->tile_mode_init == -1 && w->tile_mode == 0) {   // a new state: auto mode may try the form again
+        w->tile_mode = -1;
+        w->tile_backoff = w->tile_skip = 0;
+    }
     w->state_version += 1;
     // uploading the staging's bytes yields exactly this state (one rank)
     w->mirror_version = w->P == 1 ? w->state_version : -1;

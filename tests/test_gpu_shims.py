@@ -98,13 +98,6 @@ def test_multi_sphere_step_drop_in():
     assert log.n == 400
 
 
-def test_single_body_entry_rejects_multi_body_scene():
-    from src.physics.time_integeration import timestep_integration
-    g, sc, model, data = _model_data("traj_multi4")
-    with pytest.raises(ValueError, match="several free bodies"):
-        timestep_integration(model, "ball1", data)
-
-
 # ---- the headless runner (src/simulate.py) ---------------------------------
 @pytest.mark.parametrize("sim,golden,steps", [("single_sphere", "traj_single_sphere", 300),
                                               ("cube_incline", "traj_single_cube", 300),

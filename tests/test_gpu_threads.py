@@ -48,6 +48,60 @@ def test_two_threads_each_with_own_worlds(rb_lib=None):
     assert not errors, errors[:3]
 
 
+def test_threads_on_two_devices_capture_while_the_other_allocates(rb_lib=None):
+    """The capture gate serialises per device (rb_capi.hip ApiScope /
+    CaptureScope): a thread replaying captured step graphs on device 0 while
+    another creates, steps and destroys worlds (hipMalloc, fills, captures)
+    on device 1 must see no failed capture and exact results on both.
+    Needs two GPUs (skipped on a one-GPU box)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    import rbhip
+    from rbhip import scenes
+    rbhip.load()
+    sc0, sc1 = scenes.flat_spheres(16, 16, seed=1), scenes.flat_spheres(12, 20, seed=2)
+    steps = 20
+    ref0, ref1 = _run(rbhip, sc0, steps), _run(rbhip, sc1, steps)
+    errors = []
+
+    def replayer():
+        try:
+            with rbhip.World(sc0, device=0) as w:
+                for it in range(200):
+                    w.set_state(sc0.qpos0, sc0.qvel0)
+                    w.step(steps)                      # a cached graph after the first iteration
+                    q, v = w.get_state()
+                    if not (np.array_equal(q.view(np.uint64), ref0[0].view(np.uint64)) and
+                            np.array_equal(v.view(np.uint64), ref0[1].view(np.uint64))):
+                        errors.append(f"device 0 iteration {it}: state differs")
+                        return
+        except Exception as e:
+            errors.append(f"device 0: {e}")
+
+    def allocator():
+        try:
+            for it in range(60):
+                with rbhip.World(sc1, device=1) as w:
+                    w.set_state(sc1.qpos0, sc1.qvel0)
+                    w.step(steps)
+                    q, v = w.get_state()
+                if not (np.array_equal(q.view(np.uint64), ref1[0].view(np.uint64)) and
+                        np.array_equal(v.view(np.uint64), ref1[1].view(np.uint64))):
+                    errors.append(f"device 1 iteration {it}: state differs")
+                    return
+        except Exception as e:
+            errors.append(f"device 1: {e}")
+
+    th = [threading.Thread(target=replayer), threading.Thread(target=allocator)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not any(t.is_alive() for t in th), "a worker thread did not finish"
+    assert not errors, errors[:3]
+
+
 def test_unchanged_set_state_is_a_no_op_and_exact(rb_lib=None):
     """rb_set_state with the bytes rb_get_state just returned (the per-frame
     caller) skips the upload; with one byte changed it uploads; results stay

@@ -173,8 +173,9 @@ def test_tile_form_declines_what_it_cannot_step(rb, monkeypatch):
 def test_tile_auto_mode_retires_after_rollback(rb, oracle16, monkeypatch):
     """Auto mode (the default; RBHIP_TILE_MIN_BODIES lowered so the small
     crowded scene qualifies): the first roll-back retires the tile form for
-    the world — every later run steps hashed, no second roll-back — and the
-    state stays bit-exact with the oracle."""
+    the world (its bins freed) — every later run steps hashed, no second
+    roll-back — and the state stays bit-exact with the oracle; an
+    rb_set_state of a new state re-arms the auto mode."""
     from rbhip import scenes
     sc = scenes.crowded_cells()
     osc = oracle16.OracleScene(sc)
@@ -189,10 +190,13 @@ def test_tile_auto_mode_retires_after_rollback(rb, oracle16, monkeypatch):
         w.step(20)
         gq, gv = w.get_state()
         st = w.stats()
+        w.set_state(sc.qpos0, sc.qvel0)
+        st2 = w.stats()
     q, v = oracle16.step(osc, sc.qpos0, sc.qvel0, 80)
     assert _same(gq, q) and _same(gv, v)
     assert st0["tile_rollbacks"] == 1 and st["tile_rollbacks"] == 1, (st0, st)
     assert st["form"] != 5 and st["tile_on"] == 0, st
+    assert st2["tile_on"] == 1, st2
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
