@@ -157,7 +157,7 @@ __device__ __forceinline__ int32_t search_coop(const StepParams<T> &p, bool acti
     // the wave wait for the loads before that work starts
     const int rl = RL >= 0 ? RL : grid_rl(p.grid.super);   // heads per line: cooperative worlds 1 (rb_capi.hip)
     const uint4 id4 = bucket_head(p.cur, b, rl);
-    Snap<T> p4[QS];
+    Snap<T> p4[QS > 0 ? QS : 1];                  // (RB_QSPEC=0: a diagnostic build)
 #pragma unroll
     for (int u = 0; u < QS; ++u) p4[u] = p.cur.pos[base + u];
     __builtin_amdgcn_sched_barrier(0);            // the bucket loads issue before the body work
