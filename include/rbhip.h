@@ -206,13 +206,16 @@ int rb_p2p_connect(rb_world *w, const void *all, int64_t len);
 
 /* Halo mode of the peer-to-peer exchange, for large shards (no reference
  * counterpart: the reference is single-process).  Instead of reading every
- * peer's whole slice, each rank pushes to each peer only its bodies whose
- * cell lies within one cell of the cell bounds of that peer's own bodies
- * (a superset of everything the peer's contact searches can reach), into
- * the peer's inbox, after the ranks have exchanged those bounds.  Two
- * kernels per step, no host work; still bit-identical to every other
- * transport.  Collective: every rank must make the same call, after
- * rb_p2p_connect and before stepping.  enable = 0 returns to full reads. */
+ * peer's whole slice, the step kernel of each rank pushes to each peer only
+ * its bodies whose new cell lies within two cells of that peer's own
+ * bodies' cell bounds of the step before (a superset of everything the
+ * peer's next contact searches can reach while no body moves more than one
+ * broadphase cell per step; one that does fails the run with RB_EDOM), into
+ * the peer's inbox; one insert kernel per step then publishes the bounds
+ * and counts and inserts what the peers pushed.  No host work; still
+ * bit-identical to every other transport.  Collective: every rank must make
+ * the same call, after rb_p2p_connect and before stepping.  enable = 0
+ * returns to full reads. */
 int rb_p2p_halo(rb_world *w, int32_t enable);
 
 /* ---- the two-ball law -------------------------------------------------- */

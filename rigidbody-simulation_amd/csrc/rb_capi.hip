@@ -155,6 +155,9 @@ int64_t next_pow2(int64_t v) {
 
 int err_to_code(int32_t bits) {
     if (bits & ERR_EXCHANGE) return fail(RB_ENODEV, "device: peer-to-peer exchange timed out (a peer rank did not reach the step)");
+    if (bits & ERR_HALO_MOVE)
+        return fail(RB_EDOM, "device: a body moved more than one broadphase cell in one step (the halo exchange "
+                             "cannot guarantee its partners; use full peer reads: rb_p2p_halo(w, 0))");
     if (bits & ERR_DOMAIN) return fail(RB_EDOM, "device: non-finite or out-of-range body position");
     if (bits & ERR_UNSUPPORTED)
         return fail(RB_EUNSUPPORTED, "device: box-involved pair within contact range with no box kernel to take it");
@@ -260,6 +263,7 @@ struct rb_world {
     bool halo = false;             // rb_p2p_halo: push only the bodies a peer can reach
     int32_t *bounds = nullptr;     // peer-to-peer: [2][BOUND_COPIES][BOUND_STRIDE] own cell bounds (step parity)
     int32_t *push_cnt = nullptr;   // halo: [P] bodies pushed to each peer this step
+    int64_t *halo_e = nullptr;     // halo: the epoch the next step kernel's pushes test against
     int64_t *epoch = nullptr;      // steps taken since connect (advanced by the step kernel)
     void **peer_snap_dev = nullptr;       // [2][P] device array: each rank's snapshot buffers
     void **peer_quat_dev = nullptr;       // box worlds: [2][P] each rank's orientation snapshots
@@ -408,6 +412,17 @@ template <typename T> StepParams<T> make_step(rb_world *w, int64_t c, double dt,
     p.err = w->err;
     p.epoch = w->p2p ? w->epoch : nullptr;
     p.bounds = w->p2p ? w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE : nullptr;   // (peer-to-peer: both modes filter by them)
+    if (w->p2p && w->halo) {                     // the step kernels push to the peers (rb_halo.hpp)
+        p.halo.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
+        p.halo.mail = reinterpret_cast<const char *>(w->flags);
+        p.halo.push_cnt = w->push_cnt;
+        p.halo.halo_e = w->halo_e;
+        p.halo.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
+        p.halo.S = w->S;
+        p.halo.timeout_ticks = 500000000;        // 5 s at 100 MHz
+        p.halo.rank = (int32_t)w->rank;
+        p.halo.P = (int32_t)w->P;
+    }
     p.plist = w->plist;
     p.plist_cnt = w->plist_cnt;
     if (w->vel[0]) {
@@ -599,6 +614,8 @@ template <typename T> HaloParams<T> make_halo(rb_world *w, int64_t c, int nsp) {
     hp.bounds = w->bounds + (c % 2) * BOUND_COPIES * BOUND_STRIDE;
     hp.bounds_reset = w->bounds + ((c + 1) % 2) * BOUND_COPIES * BOUND_STRIDE;
     hp.push_cnt = w->push_cnt;
+    hp.halo_e = w->halo_e;
+    hp.own = dp<Snap<T>>(w->snap[c % 2], 0);
     hp.peer_mail = reinterpret_cast<char *const *>(w->peer_flags_dev);
     hp.mail = reinterpret_cast<const char *>(w->flags);
     hp.lay = MailLayout::make(w->P, w->S, w->esz, w->boxes);
@@ -1335,6 +1352,14 @@ int enqueue_steps(rb_world *w, int64_t nsteps, double dt, double e, double mu, d
         int rc = prime(w, dt, e, mu);
         if (rc) return rc;
     }
+    if (sharded && w->p2p && w->halo) {
+        // the halo pushes of the run's first step test against the bounds of
+        // the current positions (the insert kernels publish them after)
+        const int nsp = w->sp();
+        const hipError_t he = w->dtype == RB_F64 ? launch_halo_prime<double>(make_halo<double>(w, w->c, nsp), w->stream)
+                                                 : launch_halo_prime<float>(make_halo<float>(w, w->c, nsp), w->stream);
+        HIPCHK(he);
+    }
     auto one = [&](hipStream_t s, int64_t c) {
         return sharded ? shard_one(w, s, c, dt, e, mu, thr) : launch_one(w, s, c, dt, e, mu, thr);
     };
@@ -1624,7 +1649,8 @@ void free_world(rb_world *w) {
     drop_graphs(w);
     if (w->comm) (void)rccl().CommDestroy(w->comm);
     for (void *q : w->ipc_opened) (void)hipIpcCloseMemHandle(q);
-    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_quat_dev, w->peer_flags_dev, w->bounds, w->push_cnt};
+    void *p2pbufs[] = {w->flags, w->epoch, w->peer_snap_dev, w->peer_quat_dev, w->peer_flags_dev, w->bounds, w->push_cnt,
+                       w->halo_e};
     for (void *b : p2pbufs)
         if (b) (void)hipFree(b);
     for (auto &pr : w->tev) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -2278,6 +2304,7 @@ int rb_p2p_halo(rb_world *w, int32_t enable) {
     HIPCHK(hipStreamSynchronize(w->stream));
     if (enable) {
         if (!w->push_cnt) HIPCHK(hipMalloc((void **)&w->push_cnt, sizeof(int32_t) * w->P));
+        if (!w->halo_e) HIPCHK(hipMalloc((void **)&w->halo_e, sizeof(int64_t)));
         if (int rc = reset_bounds(w)) return rc;
         WCHK(wfill(w, w->push_cnt, 0, sizeof(int32_t) * w->P));
     }

@@ -17,6 +17,7 @@ enum : int32_t {
                                 // since box worlds, sharded or not, always launch one)
     ERR_DOMAIN = 8,             // non-finite / out-of-range position
     ERR_EXCHANGE = 16,          // peer-to-peer exchange: a peer's step did not arrive in time
+    ERR_HALO_MOVE = 32,         // halo exchange: a body moved more than one broadphase cell in one step
 };
 
 // Step-start snapshot of one body, indexed by global body id: position and
@@ -128,6 +129,66 @@ template <typename T> struct Grid {
                                        // bits 25-26: log2 of the heads per line (Table)
 };
 
+// Halo exchange (rb_p2p.hip, rb_halo.hpp), for large shards: instead of
+// reading every peer's whole slice, each rank PUSHES to each peer only its
+// bodies that may come within reach of that peer's bodies — a superset of
+// every body the peer's 2x2x2 searches can reach.
+//
+// The own bounds are accumulated by the step kernel with atomic min/max into
+// BOUND_COPIES spread copies (block b uses copy b % BOUND_COPIES, so the
+// atomics do not contend on one line), reduced and published by the insert
+// kernel (or, before a run's first step, the prime kernel).
+constexpr int BOUND_COPIES = 64;
+constexpr int BOUND_STRIDE = 32;       // int32 per copy (128 B): min x y z, max x y z, unused
+//
+// Each rank's mailbox is one uncached allocation, written by the peers over
+// xGMI (IPC mappings) and polled / read by this rank:
+//   int64  flags[P]             full-read exchange: "step e done" from peer q
+//   int64  box[P][6]            halo: peer q's cell bounds, ((e + 1) << 32) | uint32(v)
+//   int64  cnt[P]               halo: bodies peer q pushed, (e << 32) | count
+//   uint32 in_ids[2][P][S]      halo: pushed ids by step parity, region q written by peer q
+//   Snap   in_snap[2][P][S]     halo: their snapshots
+//   T      in_quat[2][P][S][4]  halo, box worlds: the orientations of pushed boxes
+// Packing the epoch into every word lets a reader tell a fresh word from a
+// stale one without a separate flag (and a release fence before it).
+struct MailLayout {
+    int64_t o_flags, o_box, o_cnt, bytes;
+    int64_t o_ids[2], o_snap[2], o_quat[2];   // o_quat: -1 without boxes
+    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz, bool boxes) {
+        MailLayout m;
+        m.o_flags = 0;
+        m.o_box = 8 * P;
+        m.o_cnt = m.o_box + 48 * P;
+        int64_t o = m.o_cnt + 8 * P;
+        for (int k = 0; k < 2; ++k) { m.o_ids[k] = o; o += 4 * P * S; }
+        o = (o + 255) / 256 * 256;
+        for (int k = 0; k < 2; ++k) { m.o_snap[k] = o; o += 4 * esz * P * S; }
+        for (int k = 0; k < 2; ++k) {
+            m.o_quat[k] = boxes ? o : -1;
+            if (boxes) o += 4 * esz * P * S;
+        }
+        m.bytes = o;
+        return m;
+    }
+};
+
+// The halo push from the step kernels (rb_halo.hpp halo_push): after its
+// bodies stepped, a wave appends each one whose new cell lies within two
+// cells of a peer's bounds of the step before (published by the peer's
+// insert kernel; a peer body moves at most one cell per step, else
+// ERR_HALO_MOVE) to that peer's inbox of the step's parity.  mail ==
+// nullptr: no push (every other transport).
+struct HaloPush {
+    char *const *peer_mail;            // [P] each peer's mailbox (own entry unused)
+    const char *mail;                  // this rank's mailbox (the peers' bounds)
+    int32_t *push_cnt;                 // [P] bodies pushed to each peer this step
+    const int64_t *halo_e;             // the epoch of the bounds this step tests against (insert / prime kernel)
+    MailLayout lay;
+    int64_t S;
+    int64_t timeout_ticks;             // s_memrealtime ticks (100 MHz) before ERR_EXCHANGE
+    int32_t rank, P;
+};
+
 template <typename T> struct StepParams {
     // the first 64 bytes hold everything the step's first loads need, so the
     // prologue fetches them with one scalar load
@@ -173,6 +234,7 @@ template <typename T> struct StepParams {
     int32_t *defer_q;
     int32_t *defer_cnt;
     int32_t *defer_reset;
+    HaloPush halo;                     // fused halo push (halo-exchanging shards)
 };
 
 static_assert(offsetof(StepParams<double>, xfrc) == 64 && offsetof(StepParams<float>, xfrc) == 64,
@@ -214,45 +276,12 @@ template <typename T> struct P2PParams {
     int32_t *bounds_reset;
 };
 
-// Halo exchange (rb_p2p.hip), for large shards: instead of reading every
-// peer's whole slice, each rank PUSHES to each peer only its bodies whose
-// cell lies within one cell of that peer's own bodies' cell bounds — a
-// superset of every body the peer's 2x2x2 searches can reach.
-//
-// The own bounds are accumulated by the step kernel with atomic min/max into
-// BOUND_COPIES spread copies (block b uses copy b % BOUND_COPIES, so the
-// atomics do not contend on one line), reduced by the push kernel.
-constexpr int BOUND_COPIES = 64;
-constexpr int BOUND_STRIDE = 32;       // int32 per copy (128 B): min x y z, max x y z, unused
-//
-// Each rank's mailbox is one uncached allocation, written by the peers over
-// xGMI (IPC mappings) and polled / read by this rank:
-//   int64  flags[P]          full-read exchange: "step e done" from peer q
-//   int64  box[P][6]         halo: peer q's cell bounds, (e << 32) | uint32(v)
-//   int64  cnt[P]            halo: bodies peer q pushed, (e << 32) | count
-//   uint32 in_ids[P][S]      halo: pushed ids, region q written by peer q
-//   Snap   in_snap[P][S]     halo: their snapshots
-//   T      in_quat[P][S][4]  halo, box worlds: the orientations of pushed boxes
-// Packing the epoch into every word lets a reader tell a fresh word from a
-// stale one without a separate flag (and a release fence before it).
-struct MailLayout {
-    int64_t o_flags, o_box, o_cnt, o_ids, o_snap, o_quat, bytes;   // o_quat: -1 without boxes
-    __host__ __device__ static MailLayout make(int64_t P, int64_t S, int64_t esz, bool boxes) {
-        MailLayout m;
-        m.o_flags = 0;
-        m.o_box = 8 * P;
-        m.o_cnt = m.o_box + 48 * P;
-        m.o_ids = m.o_cnt + 8 * P;
-        m.o_snap = (m.o_ids + 4 * P * S + 255) / 256 * 256;
-        m.o_quat = boxes ? m.o_snap + 4 * esz * P * S : -1;
-        m.bytes = m.o_snap + (boxes ? 8 : 4) * esz * P * S;
-        return m;
-    }
-};
-
+// The halo exchange's kernels after the step kernel (insert) and before a
+// run's first step (prime)
 template <typename T> struct HaloParams {
     InsertParams<T> ins;               // the local next snapshot's table (count, skip unused)
     Snap<T> *dst;                      // the local next snapshot (own rows fresh; pushed rows land here)
+    const Snap<T> *own;                // prime: the current snapshot (own rows)
     int32_t *bounds;                   // this step's own-bound copies (from the step kernel)
     int32_t *bounds_reset;             // the other parity's copies: reset for the next step kernel
     int32_t *push_cnt;                 // [P] bodies pushed to each peer this step
@@ -260,6 +289,7 @@ template <typename T> struct HaloParams {
     const char *mail;                  // this rank's mailbox
     MailLayout lay;
     const int64_t *epoch;
+    int64_t *halo_e;                   // written for the next step kernel's pushes
     int32_t rank, P, n_local;
     int64_t lo, S;
     int64_t timeout_ticks;
@@ -372,6 +402,7 @@ template <typename T> hipError_t launch_state_out(const StateIO<T> &p, bool want
 template <typename T> hipError_t launch_state_out_flat(const StateIO<T> &p, bool want_q, bool want_v, hipStream_t s);
 template <typename T> hipError_t launch_p2p_exchange(const P2PParams<T> &p, hipStream_t s);   // rb_p2p.hip
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s); // rb_p2p.hip
+template <typename T> hipError_t launch_halo_prime(const HaloParams<T> &p, hipStream_t s);    // rb_p2p.hip
 hipError_t launch_publish_err(const int32_t *err, int32_t *host_dev, hipStream_t s,              // rb_p2p.hip
                               const int32_t *why = nullptr, const unsigned long long *commits = nullptr,
                               int64_t *host_tile_dev = nullptr);

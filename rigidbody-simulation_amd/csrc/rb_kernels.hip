@@ -53,6 +53,7 @@ __device__ unsigned long long rb_stamp_buf[1 << 16][16];
 
 #include "rb_boxes.hpp"
 #include "rb_grid.hpp"
+#include "rb_halo.hpp"
 #include "rb_internal.hpp"
 #include "rb_body.hpp"
 
@@ -473,6 +474,10 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     STAMP(4);
 
     // ---- K3: integrate (collision.py:90-100) ---------------------------------
+    if (p.bounds) {                              // peer-to-peer exchange: the step-start cell too
+        int32_t cx, cy, cz;
+        if (cell_of(x.x, x.y, x.z, p.grid.inv_cs, cx, cy, cz)) { cell[3] = cx; cell[4] = cy; cell[5] = cz; }
+    }
     x = {x.x + v.x * p.dt, x.y + v.y * p.dt, x.z + v.z * p.dt};
     Snap<T> sn;
     sn.x = x.x; sn.y = x.y; sn.z = x.z; sn.r = bi;
@@ -488,7 +493,7 @@ __device__ __forceinline__ void body_update(const StepParams<T> &p, int32_t l, i
     constexpr int RL = PM == 1 ? 0 : PM == 2 ? 2 : -1;
     if (p.next.line) cl = claim_slot<L, RL>(p.grid, p.next, p.err, sn, gen_next);
     wt_store(p.snap_next + i, sn);
-    if (p.bounds) {                              // halo exchange: this body's new cell
+    if (p.bounds) {                              // peer-to-peer exchange: this body's new cell
         int32_t cx, cy, cz;
         if (cell_of(sn.x, sn.y, sn.z, p.grid.inv_cs, cx, cy, cz)) { cell[0] = cx; cell[1] = cy; cell[2] = cz; }
     }
@@ -807,12 +812,17 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
 
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
+    const int64_t halo_e = p.halo.mail ? *p.halo.halo_e : 0;   // (halo-exchanging shards: the push's epoch)
     const bool active = lb < ld.n_local;
-    int32_t cell[3] = {INT32_MAX, 0, 0};
+    int32_t cell[6] = {INT32_MAX, 0, 0, 0, 0, 0};   // new cell, step-start cell (peer-to-peer exchange)
     if (G > 1 || HELP || active)                 // (a helper's barriers: every lane)
         body_step<T, MAXP, G, WIDE, BOXES, true, HELP>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand,
                                                        cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, help_lds);
     if (p.bounds) fold_bounds(p.bounds, cell);
+    if (p.halo.mail) {                           // halo-exchanging shard: push to the peers
+        int32_t b[6];
+        if (halo_bounds(p, halo_e, b)) halo_push(p, halo_e, cell[0] != INT32_MAX, (int32_t)(ld.lo + lb), cell, b);
+    }
     if (blockIdx.x == 0 && tid == 0) {
         if (p.next.line) *p.next.gen = *p.cur.gen + 1u;
         if (p.epoch) *p.epoch += 1;
@@ -873,11 +883,21 @@ void box_kernel(StepParams<T> p) {
     const uint32_t gen = *p.cur.gen;
     const int32_t n = *p.defer_cnt;
     int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
-    for (int64_t qi = (int64_t)blockIdx.x * STEP_BLOCK + tid; qi < n; qi += (int64_t)gridDim.x * STEP_BLOCK) {
-        int32_t cell[3] = {INT32_MAX, 0, 0};
+    // halo-exchanging shard: the peers' bounds, read with every lane active
+    int32_t hb[6];
+    const int64_t halo_e = p.halo.mail ? *p.halo.halo_e : 0;
+    const bool halo = p.halo.mail && n > (int32_t)(blockIdx.x * STEP_BLOCK) && halo_bounds(p, halo_e, hb);
+    for (int64_t qi0 = (int64_t)blockIdx.x * STEP_BLOCK; qi0 < n; qi0 += (int64_t)gridDim.x * STEP_BLOCK) {
+        const int64_t qi = qi0 + tid;
+        int32_t cell[6] = {INT32_MAX, 0, 0, 0, 0, 0};
+        int32_t l = 0;
         // one lane per body: the lane's LDS column (partner list, polygon) is slot = tid
-        body_step<T, MAXP, 1, false, true>(p, Lead<T>::of(p), true, p.defer_q[qi], tid, 0, tid, s_id, nullptr, nullptr, nullptr, nullptr,
-                                           cell, gen, s_poly);
+        if (qi < n) {
+            l = p.defer_q[qi];
+            body_step<T, MAXP, 1, false, true>(p, Lead<T>::of(p), true, l, tid, 0, tid, s_id, nullptr, nullptr, nullptr,
+                                               nullptr, cell, gen, s_poly);
+        }
+        if (halo) halo_push(p, halo_e, cell[0] != INT32_MAX, p.lo + l, cell, hb);   // (every lane of the wave)
         if (cell[0] != INT32_MAX)
 #pragma unroll
             for (int d = 0; d < 3; ++d) { lo[d] = min(lo[d], cell[d]); hi[d] = max(hi[d], cell[d]); }
@@ -946,8 +966,9 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
     const int tid = threadIdx.x;
     const int64_t gt = (int64_t)blockIdx.x * STEP_BLOCK + tid;
     const int64_t lb = gt;
-    int32_t cell[3] = {INT32_MAX, 0, 0};
+    int32_t cell[6] = {INT32_MAX, 0, 0, 0, 0, 0};
     const uint32_t gen_next = *p.cur.gen + 1u;
+    const int64_t halo_e = p.halo.mail ? *p.halo.halo_e : 0;
     if (p.next.line && blockIdx.x == 0 && tid == 0) *p.next.gen = gen_next;
     if (lb < p.n_local) {
         const int32_t l = (int32_t)lb, i = p.lo + l;
@@ -965,6 +986,10 @@ __global__ __launch_bounds__(STEP_BLOCK) void update_kernel(StepParams<T> p) {
                           cell, gen_next);
     }
     if (p.bounds) fold_bounds(p.bounds, cell);
+    if (p.halo.mail) {                           // halo-exchanging shard: push to the peers
+        int32_t b[6];
+        if (halo_bounds(p, halo_e, b)) halo_push(p, halo_e, cell[0] != INT32_MAX, (int32_t)(p.lo + lb), cell, b);
+    }
 }
 
 #if RB_STAMPS

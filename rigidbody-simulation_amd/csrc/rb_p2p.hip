@@ -19,36 +19,9 @@
 // exchange (which overwrites this parity) only after every peer has flagged
 // step t+1, i.e. finished reading it: no further synchronisation is needed.
 // Replaces, per step, the all-gather + insert of the RCCL transport.
-#include "rb_grid.hpp"
+#include "rb_halo.hpp"
 
 namespace rb {
-
-// System-scope word accesses: they bypass the caches on both sides, so data
-// another GPU wrote (or will read) needs no cache maintenance — no L2
-// writeback or invalidate (a fence per wave or block at agent/system scope
-// costs an L2 writeback/invalidate each: measured +9-13 us per step at C3).
-__device__ __forceinline__ int64_t load_sys(const int64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void store_sys(int64_t *p, int64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-template <typename T> __device__ __forceinline__ Snap<T> load_snap_sys(const Snap<T> *p) {
-    const T *w = &p->x;
-    Snap<T> s;
-    s.x = __hip_atomic_load(w + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    s.y = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    s.z = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    s.r = __hip_atomic_load(w + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return s;
-}
-template <typename T> __device__ __forceinline__ void store_snap_sys(Snap<T> *p, const Snap<T> &s) {
-    T *w = &p->x;
-    __hip_atomic_store(w + 0, s.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(w + 1, s.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(w + 2, s.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(w + 3, s.r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // a box's orientation row (w x y z) from another GPU's memory
 template <typename T> __device__ __forceinline__ void copy_quat_sys(T *dst, const T *src) {
@@ -123,32 +96,28 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
 }
 
 // ---- halo exchange (large shards) -----------------------------------------
-// Two kernels after the step kernel of step e (HaloParams, rb_internal.hpp):
-//   push:   block 0 reduces the own cell bounds and stores them, epoch-tagged,
-//           into every peer's mailbox (and resets the other parity's copies);
-//           every block waits for all peers' bounds of step e, then each
-//           thread tests one own body's new cell against each peer's bounds
-//           +-1 cell and, if inside, appends (id, snapshot) to that peer's
-//           inbox (slot from a wave-aggregated atomic on push_cnt[peer]),
-//           with a box's orientation in box worlds;
-//           each wave ends with a system-scope release (its remote stores
-//           complete before the kernel does);
-//   insert: block 0 stores push_cnt[q], epoch-tagged, into peer q's mailbox
-//           and resets it; every block waits for all peers' counts of step
-//           e, then the grid copies the received snapshots into the next
-//           snapshot buffer and inserts them into the next table.
-// A peer pushes into this rank's inbox for step e+1 only after this rank's
-// bounds of step e+1 reached it, i.e. after this rank's insert of step e
-// finished reading: one inbox per peer suffices.
-// Why exact: a partner j of an own body i lies within reach of i, and the
-// cell size is >= 2 x the reach, so cell(j) is within one cell of cell(i)
-// on every axis — inside the bounds +-1 of i's rank.  Bodies not pushed are
-// never within reach of any body of the receiving rank, and every contact
-// test and its order depend only on the bodies within reach.
-
-__device__ __forceinline__ uint64_t pack_epoch(int64_t e, int32_t v) {
-    return ((uint64_t)e << 32) | (uint32_t)v;
-}
+// The step kernel of step e pushes (rb_halo.hpp halo_push): each wave waits
+// for the peers' bounds of the step before (published by their insert or
+// prime kernels), then appends each own body whose new cell lies within two
+// cells of a peer's bounds to that peer's inbox of parity e & 1 (slot from a
+// wave-aggregated atomic on push_cnt[peer]), with a box's orientation in box
+// worlds, and completes its remote stores before the kernel ends.  Then
+//   insert: block 0 reduces the own cell bounds the step kernel folded and
+//           stores them, tagged e + 1, into every peer's mailbox (for the
+//           peers' next pushes), stores push_cnt[q], tagged e, into peer q's
+//           mailbox and resets it, and hands e to the next step kernel
+//           (halo_e); every block waits for all peers' counts of step e,
+//           then the grid copies the received snapshots (inbox parity e & 1)
+//           into the next snapshot buffer and inserts them into the next
+//           table;
+//   prime:  before a run's first step, the bounds of the current positions,
+//           tagged (steps taken) + 1, and halo_e, as an insert kernel of the
+//           step before would have left them.
+// A peer pushes into this rank's inbox of parity e & 1 again only at step
+// e + 2, after this rank's bounds of step e + 1 reached it — published by
+// this rank's insert kernel of step e + 1, after its insert of step e
+// finished reading: two inboxes (by parity) suffice.
+// Why exact: rb_halo.hpp halo_push.
 
 // One lane per peer (lanes 0..63 of the block) waits until word(q) of every
 // peer q != rank carries epoch >= e.  Bounded: after timeout_ticks (or once
@@ -172,97 +141,23 @@ __device__ __forceinline__ void wait_peers(int32_t P, int32_t rank, int64_t e, i
     }
 }
 
-
-template <typename T>
-__global__ __launch_bounds__(256) void halo_push_kernel(HaloParams<T> p) {
-    const int64_t e = *p.epoch;
+// the own cell bounds (lane k folds copy k; the butterfly leaves them in
+// every lane), stored tagged into the peers' mailboxes by lanes q < P
+template <typename T> __device__ __forceinline__ void publish_bounds(const HaloParams<T> &p, int32_t (&b)[6],
+                                                                     int64_t tag) {
     const int tid = threadIdx.x;
-    const MailLayout &L = p.lay;
-    __shared__ int32_t s_box[64][6];
-    if (blockIdx.x == 0 && tid < 64) {
-        // own bounds: lane k folds copy k; the butterfly leaves the result in every lane
-        const int32_t *c = p.bounds + (int64_t)tid * BOUND_STRIDE;
-        int32_t b[6];
 #pragma unroll
-        for (int d = 0; d < 6; ++d) b[d] = c[d];
+    for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1)
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                b[d] = min(b[d], __shfl_xor(b[d], off));
-                b[3 + d] = max(b[3 + d], __shfl_xor(b[3 + d], off));
-            }
-        int32_t *r = p.bounds_reset + (int64_t)tid * BOUND_STRIDE;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) { r[d] = INT32_MAX; r[3 + d] = INT32_MIN; }
-        if (tid < p.P && tid != p.rank) {
-            int64_t *box = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_box) + 6 * p.rank;
-#pragma unroll
-            for (int d = 0; d < 6; ++d) store_sys(box + d, (int64_t)pack_epoch(e, b[d]));
+        for (int d = 0; d < 3; ++d) {
+            b[d] = min(b[d], __shfl_xor(b[d], off));
+            b[3 + d] = max(b[3 + d], __shfl_xor(b[3 + d], off));
         }
-    }
-    const int64_t *box_in = reinterpret_cast<const int64_t *>(p.mail + L.o_box);
-    wait_peers(p.P, p.rank, e, p.timeout_ticks, p.ins.err, [&](int q) {
-        int64_t lo = INT64_MAX;
+    if (tid < p.P && tid != p.rank) {
+        int64_t *box = reinterpret_cast<int64_t *>(p.peer_mail[tid] + p.lay.o_box) + 6 * p.rank;
 #pragma unroll
-        for (int d = 0; d < 6; ++d) {
-            const int64_t w = (int64_t)((uint64_t)load_sys(box_in + 6 * q + d) >> 32);
-            lo = w < lo ? w : lo;
-        }
-        return lo;
-    });
-    if (tid < 64 && tid < p.P && tid != p.rank)
-#pragma unroll
-        for (int d = 0; d < 6; ++d) s_box[tid][d] = (int32_t)(uint32_t)load_sys(box_in + 6 * tid + d);
-    __syncthreads();
-
-    const int64_t l = (int64_t)blockIdx.x * 256 + tid;
-    const bool active = l < p.n_local;
-    int32_t cx = 0, cy = 0, cz = 0;
-    Snap<T> s{};
-    bool ok = false, box = false;
-    if (active) {
-        s = p.dst[p.lo + l];
-        ok = cell_of(s.x, s.y, s.z, p.ins.grid.inv_cs, cx, cy, cz);   // else: ERR_DOMAIN raised by the step
-        box = p.quat && p.ins.kind[p.lo + l] != 0;
+        for (int d = 0; d < 6; ++d) store_sys(box + d, (int64_t)pack_epoch(tag, b[d]));
     }
-    const uint64_t lt = (1ull << (tid & 63)) - 1ull;
-    bool pushed = false;                          // wave-uniform
-    for (int q = 0; q < p.P; ++q) {
-        if (q == p.rank) continue;
-        const int32_t *b = s_box[q];
-        // empty bounds (min > max): the peer owns no body, needs none.
-        // Compared in int64: min - 1 / max + 1 cannot overflow.
-        const bool in = ok && b[0] <= b[3] && (int64_t)cx >= (int64_t)b[0] - 1 && (int64_t)cx <= (int64_t)b[3] + 1 &&
-                        (int64_t)cy >= (int64_t)b[1] - 1 && (int64_t)cy <= (int64_t)b[4] + 1 &&
-                        (int64_t)cz >= (int64_t)b[2] - 1 && (int64_t)cz <= (int64_t)b[5] + 1;
-        const uint64_t m = __ballot(in);
-        if (m == 0) continue;
-        pushed = true;
-        const int leader = __builtin_ctzll(m);
-        int32_t base = 0;
-        if ((tid & 63) == leader) base = atomicAdd(p.push_cnt + q, __popcll(m));
-        base = __shfl(base, leader);
-        if (in) {
-            const int64_t slot = base + __popcll(m & lt);
-            if (slot < p.S) {       // a peer holds at most S of this rank's bodies
-                char *mail = p.peer_mail[q];
-                uint32_t *ids = reinterpret_cast<uint32_t *>(mail + L.o_ids) + (int64_t)p.rank * p.S;
-                Snap<T> *sn = reinterpret_cast<Snap<T> *>(mail + L.o_snap) + (int64_t)p.rank * p.S;
-                __hip_atomic_store(ids + slot, (uint32_t)(p.lo + l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                store_snap_sys(sn + slot, s);
-                if (box) {                        // a box: its orientation too
-                    T *qm = reinterpret_cast<T *>(mail + L.o_quat) + 4 * ((int64_t)p.rank * p.S + slot);
-                    const T *qs = p.quat + 4 * (p.lo + l);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) __hip_atomic_store(qm + k, qs[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-            }
-        }
-    }
-    // the pushes are complete (acknowledged by the peer's memory) before
-    // this kernel is, so before the insert kernel publishes their count
-    if (pushed) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): no cache writeback needed
 }
 
 template <typename T>
@@ -271,11 +166,22 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
     const int tid = threadIdx.x;
     const MailLayout &L = p.lay;
     __shared__ int64_t s_off[65];
-    if (blockIdx.x == 0 && tid < p.P && tid != p.rank) {
-        const int32_t n = p.push_cnt[tid];
-        int64_t *cnt = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_cnt) + p.rank;
-        store_sys(cnt, (int64_t)pack_epoch(e, n < p.S ? n : (int32_t)p.S));
-        p.push_cnt[tid] = 0;
+    if (blockIdx.x == 0 && tid < 64) {
+        const int32_t *c = p.bounds + (int64_t)tid * BOUND_STRIDE;
+        int32_t b[6];
+#pragma unroll
+        for (int d = 0; d < 6; ++d) b[d] = c[d];
+        int32_t *r = p.bounds_reset + (int64_t)tid * BOUND_STRIDE;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { r[d] = INT32_MAX; r[3 + d] = INT32_MIN; }
+        publish_bounds(p, b, e + 1);
+        if (tid < p.P && tid != p.rank) {
+            const int32_t n = p.push_cnt[tid];
+            int64_t *cnt = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_cnt) + p.rank;
+            store_sys(cnt, (int64_t)pack_epoch(e, n < p.S ? n : (int32_t)p.S));
+            p.push_cnt[tid] = 0;
+        }
+        if (tid == 0) *p.halo_e = e;
     }
     const int64_t *cnt_in = reinterpret_cast<const int64_t *>(p.mail + L.o_cnt);
     wait_peers(p.P, p.rank, e, p.timeout_ticks, p.ins.err,
@@ -294,8 +200,9 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
     }
     __syncthreads();
     const int64_t total = s_off[p.P];
-    const uint32_t *ids = reinterpret_cast<const uint32_t *>(p.mail + L.o_ids);
-    const Snap<T> *sn = reinterpret_cast<const Snap<T> *>(p.mail + L.o_snap);
+    const int par = (int)(e & 1);
+    const uint32_t *ids = reinterpret_cast<const uint32_t *>(p.mail + L.o_ids[par]);
+    const Snap<T> *sn = reinterpret_cast<const Snap<T> *>(p.mail + L.o_snap[par]);
     const uint32_t gen = *p.ins.tab.gen;
     for (int64_t k = (int64_t)blockIdx.x * 256 + tid; k < total; k += (int64_t)gridDim.x * 256) {
         int q = 0;
@@ -309,18 +216,56 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
         }
         p.dst[id] = s;
         const bool box = p.ins.kind[id] != 0;
-        if (box && p.quat) copy_quat_sys(p.quat + 4 * (int64_t)id, reinterpret_cast<const T *>(p.mail + L.o_quat) + 4 * o);
+        if (box && p.quat) copy_quat_sys(p.quat + 4 * (int64_t)id, reinterpret_cast<const T *>(p.mail + L.o_quat[par]) + 4 * o);
         insert_id(p.ins.grid, p.ins.tab, p.ins.err, s, id | (box ? BOX_FLAG : 0u), gen);
+    }
+}
+
+// one block: the own bodies' current cells folded, published tagged
+// (steps taken) + 1; halo_e = steps taken
+template <typename T>
+__global__ __launch_bounds__(256) void halo_prime_kernel(HaloParams<T> p) {
+    const int64_t e = *p.epoch;
+    const int tid = threadIdx.x;
+    int32_t lo[3] = {INT32_MAX, INT32_MAX, INT32_MAX}, hi[3] = {INT32_MIN, INT32_MIN, INT32_MIN};
+    for (int64_t l = tid; l < p.n_local; l += 256) {
+        const Snap<T> s = p.own[p.lo + l];
+        int32_t c[3];
+        if (!cell_of(s.x, s.y, s.z, p.ins.grid.inv_cs, c[0], c[1], c[2])) continue;   // (the step raises ERR_DOMAIN)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) { lo[d] = min(lo[d], c[d]); hi[d] = max(hi[d], c[d]); }
+    }
+    __shared__ int32_t s_b[4][6];
+    int32_t b[6] = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            b[d] = min(b[d], __shfl_xor(b[d], off));
+            b[3 + d] = max(b[3 + d], __shfl_xor(b[3 + d], off));
+        }
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) s_b[tid >> 6][d] = b[d];
+    __syncthreads();
+    if (tid < 64) {
+#pragma unroll
+        for (int d = 0; d < 6; ++d) b[d] = s_b[tid & 3][d];   // publish_bounds folds the four waves' results
+        publish_bounds(p, b, e + 1);
+        if (tid == 0) *p.halo_e = e;
     }
 }
 
 template <typename T> hipError_t launch_halo_exchange(const HaloParams<T> &p, hipStream_t s) {
     if (p.P < 1 || p.P > 64 || p.S <= 0) return hipErrorInvalidValue;
-    const int64_t pb = (p.n_local + 255) / 256;
-    hipLaunchKernelGGL((halo_push_kernel<T>), dim3((unsigned)(pb > 0 ? pb : 1)), dim3(256), 0, s, p);
     int64_t ib = ((int64_t)(p.P - 1) * p.S + 255) / 256;
     ib = ib < 1 ? 1 : ib > 256 ? 256 : ib;
     hipLaunchKernelGGL((halo_insert_kernel<T>), dim3((unsigned)ib), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+template <typename T> hipError_t launch_halo_prime(const HaloParams<T> &p, hipStream_t s) {
+    if (p.P < 1 || p.P > 64 || p.S <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((halo_prime_kernel<T>), dim3(1), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -335,6 +280,8 @@ template hipError_t launch_p2p_exchange<double>(const P2PParams<double> &, hipSt
 template hipError_t launch_p2p_exchange<float>(const P2PParams<float> &, hipStream_t);
 template hipError_t launch_halo_exchange<double>(const HaloParams<double> &, hipStream_t);
 template hipError_t launch_halo_exchange<float>(const HaloParams<float> &, hipStream_t);
+template hipError_t launch_halo_prime<double>(const HaloParams<double> &, hipStream_t);
+template hipError_t launch_halo_prime<float>(const HaloParams<float> &, hipStream_t);
 
 }  // namespace rb
 

@@ -187,3 +187,40 @@ def test_p2p_exchange_times_out_instead_of_hanging(tmp_path, halo):
     msg = open(out).read()
     assert "exchange timed out" in msg, msg
     assert time.time() - t0 < 60
+
+
+def _halo_move_worker(rank, P, port, out):
+    for pth in (ROOT, PKG):
+        sys.path.insert(0, pth)
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    import rbhip
+    from rbhip import scenes
+    from rbhip.shard import ShardedWorld
+    sc = scenes.tiled(scenes.flat_spheres, P, 8, 8, seed=1)
+    v0 = sc.qvel0.copy()
+    v0[3, 0] = 200.0                   # rank 0's body 3: 2 m per step, five cells
+    sw = ShardedWorld(sc.with_(qvel0=v0), device=0, transport="p2p", halo=True)
+    msg = "no error"
+    try:
+        sw.step(3)
+        sw.sync()
+    except rbhip.RbError as e:
+        msg = str(e)
+    if rank == 0:
+        with open(out, "w") as f:
+            f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_halo_push_raises_when_a_body_moves_more_than_a_cell(tmp_path):
+    """The halo push (rb_halo.hpp) is exact only while no body moves more
+    than one broadphase cell per step: a body that does raises an error on
+    its rank (RB_EDOM), not a silent pass."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "msg.txt")
+    mp.start_processes(_halo_move_worker, args=(2, _free_port(), out), nprocs=2, start_method="spawn")
+    msg = open(out).read()
+    assert "more than one broadphase cell" in msg, msg
