@@ -1,11 +1,15 @@
 """Diagnostic: per-step cost of the sharded stepping loop's pieces on one
-GPU (host launch overhead vs device time), C2 scene.  Not part of the
-product; results go to stdout."""
+GPU (host launch overhead vs device time), C2 scene (CFG=..., or NX, NY for
+a flat NX x NY scene; LIB=path loads another build of the library, for
+A/Bs).  Not part of the product; results go to stdout."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rigidbody-simulation_amd"))
 import torch
 torch.cuda.init()
+from rbhip import _lib
+if os.environ.get("LIB"):
+    _lib.load(os.environ["LIB"])
 import rbhip
 from rbhip import scenes
 from rbhip.shard import wrap_gpos

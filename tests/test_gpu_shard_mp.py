@@ -104,6 +104,28 @@ def test_inlibrary_exchange_one_rank_matches_world(scene):
     assert np.array_equal(q1, q2) and np.array_equal(v1, v2)
 
 
+@pytest.mark.parametrize("halo", [False, True])
+def test_p2p_one_rank_matches_world(halo):
+    """The peer-to-peer exchange with one rank (the graph of step kernel and
+    exchange kernels, the halo mode's prime, push tail and insert kernel,
+    with no peer data): the same state as rb_step, eager, one graph and a
+    chunked replay."""
+    import rbhip
+    from rbhip import scenes
+    sc = scenes.flat_spheres(24, 24, seed=5)
+    with rbhip.World(sc) as ref:
+        ref.step(613)
+        q1, v1 = ref.get_state()
+    with rbhip.World(sc) as w:
+        w.p2p_connect(w.p2p_handles())
+        w.p2p_halo(halo)
+        for n in (1, 12, 600):
+            w.shard_run(n)
+        w.sync()
+        q2, v2 = w.get_state()
+    assert np.array_equal(q1, q2) and np.array_equal(v1, v2)
+
+
 def test_inlibrary_exchange_requires_comm():
     import rbhip
     from rbhip import scenes
