@@ -771,7 +771,10 @@ __device__ __forceinline__ void help_body(const StepParams<T> &p, const Lead<T> 
     if (!WIDE) __syncthreads();                  // search_coop's two barriers
 }
 
-template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false, bool HELP = false>
+// HALO: the halo push compiled in (checked at run time: p.halo.mail); the
+// wide forms — the single-GPU bench's kernels — are also instantiated
+// without it (launch_step_wide picks), which measured 1-2 % faster at C3
+template <typename T, int MAXP, int G, bool WIDE = false, bool BOXES = false, bool HELP = false, bool HALO = true>
 __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> &ld) {
     constexpr int NB = STEP_BLOCK / G;          // bodies per workgroup
     __shared__ int32_t s_id[MAXP * NB];
@@ -812,14 +815,14 @@ __device__ __forceinline__ void step_body(const StepParams<T> &p, const Lead<T> 
 
     const int slot = tid / G, k = tid % G;
     const int64_t lb = (int64_t)xcd_block(blockIdx.x, gridDim.x) * NB + slot;
-    const int64_t halo_e = p.halo.mail ? *p.halo.halo_e : 0;   // (halo-exchanging shards: the push's epoch)
+    const int64_t halo_e = HALO && p.halo.mail ? *p.halo.halo_e : 0;   // (halo-exchanging shards: the push's epoch)
     const bool active = lb < ld.n_local;
     int32_t cell[6] = {INT32_MAX, 0, 0, 0, 0, 0};   // new cell, step-start cell (peer-to-peer exchange)
     if (G > 1 || HELP || active)                 // (a helper's barriers: every lane)
         body_step<T, MAXP, G, WIDE, BOXES, true, HELP>(p, ld, active, lb, slot, k, tid, s_id, s_pos, t_id, t_pos, s_cand,
                                                        cell, 0u /* loaded in body_step */, s_poly, s_didx, s_hpos, help_lds);
     if (p.bounds) fold_bounds(p.bounds, cell);
-    if (p.halo.mail) {                           // halo-exchanging shard: push to the peers
+    if (HALO && p.halo.mail) {                   // halo-exchanging shard: push to the peers
         int32_t b[6];
         if (halo_bounds(p, halo_e, b)) halo_push(p, halo_e, cell[0] != INT32_MAX, (int32_t)(ld.lo + lb), cell, b);
     }
@@ -908,21 +911,21 @@ void box_kernel(StepParams<T> p) {
     if (blockIdx.x == 0 && tid == 0) *p.defer_reset = 0;    // the next step's queue
 }
 // one wave per SIMD (up to 64 x 1024 owned bodies): every register is free
-template <typename T, int MAXP>
+template <typename T, int MAXP, bool HALO>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void step_kernel_wide(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
                       const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
-    step_body<T, MAXP, 1, true, false>(
+    step_body<T, MAXP, 1, true, false, false, HALO>(
         p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
 }
 
 // the wide form with a helper wave per workgroup (help_body): two waves per
 // SIMD, each within 256 registers
-template <typename T, int MAXP>
+template <typename T, int MAXP, bool HALO>
 __global__ __launch_bounds__(2 * STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void step_kernel_wide_help(const Snap<T> *snap_cur, T *st_base, int64_t st_S, const T *cs_base, int64_t cs_Npad,
                            const int32_t *cs_kind, int32_t n_local, int32_t lo, StepParams<T> p) {
-    step_body<T, MAXP, 1, true, false, true>(
+    step_body<T, MAXP, 1, true, false, true, HALO>(
         p, Lead<T>{snap_cur, BodyState<T>{st_base, st_S}, BodyConsts<T>{cs_base, cs_Npad, cs_kind}, n_local, lo});
 }
 
@@ -1255,13 +1258,27 @@ template <typename T> hipError_t launch_kat_narrow(int64_t n, const double *in, 
 template <typename T> hipError_t launch_step_wide(const StepParams<T> &p, int maxp, bool help, hipStream_t s) {
     int64_t blocks = (p.n_local + STEP_BLOCK - 1) / STEP_BLOCK;
     if (blocks < 1) blocks = 1;
+    const bool halo = p.halo.mail != nullptr;
+#define RB_WIDE_LAUNCH(K, M, H, TH)                                                                               \
+    hipLaunchKernelGGL((K<T, M, H>), dim3((unsigned)blocks), dim3(TH), 0, s, LEAD_ARGS(p), p)
     if (help) {
-        if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide_help<T, 16>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
-        else hipLaunchKernelGGL((step_kernel_wide_help<T, 32>), dim3((unsigned)blocks), dim3(2 * STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+        if (maxp <= 16) {
+            if (halo) RB_WIDE_LAUNCH(step_kernel_wide_help, 16, true, 2 * STEP_BLOCK);
+            else RB_WIDE_LAUNCH(step_kernel_wide_help, 16, false, 2 * STEP_BLOCK);
+        } else {
+            if (halo) RB_WIDE_LAUNCH(step_kernel_wide_help, 32, true, 2 * STEP_BLOCK);
+            else RB_WIDE_LAUNCH(step_kernel_wide_help, 32, false, 2 * STEP_BLOCK);
+        }
         return hipGetLastError();
     }
-    if (maxp <= 16) hipLaunchKernelGGL((step_kernel_wide<T, 16>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
-    else hipLaunchKernelGGL((step_kernel_wide<T, 32>), dim3((unsigned)blocks), dim3(STEP_BLOCK), 0, s, LEAD_ARGS(p), p);
+    if (maxp <= 16) {
+        if (halo) RB_WIDE_LAUNCH(step_kernel_wide, 16, true, STEP_BLOCK);
+        else RB_WIDE_LAUNCH(step_kernel_wide, 16, false, STEP_BLOCK);
+    } else {
+        if (halo) RB_WIDE_LAUNCH(step_kernel_wide, 32, true, STEP_BLOCK);
+        else RB_WIDE_LAUNCH(step_kernel_wide, 32, false, STEP_BLOCK);
+    }
+#undef RB_WIDE_LAUNCH
     return hipGetLastError();
 }
 
