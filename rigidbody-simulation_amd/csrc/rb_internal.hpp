@@ -145,7 +145,7 @@ constexpr int BOUND_STRIDE = 32;       // int32 per copy (128 B): min x y z, max
 // xGMI (IPC mappings) and polled / read by this rank:
 //   int64  flags[P]             full-read exchange: "step e done" from peer q
 //   int64  box[P][6]            halo: peer q's cell bounds, ((e + 1) << 32) | uint32(v)
-//   int64  cnt[P]               halo: bodies peer q pushed, (e << 32) | count
+//   int64  cnt[2][P]            halo: bodies peer q pushed, (e << 32) | count, by step parity
 //   uint32 in_ids[2][P][S]      halo: pushed ids by step parity, region q written by peer q
 //   Snap   in_snap[2][P][S]     halo: their snapshots
 //   T      in_quat[2][P][S][4]  halo, box worlds: the orientations of pushed boxes
@@ -159,7 +159,7 @@ struct MailLayout {
         m.o_flags = 0;
         m.o_box = 8 * P;
         m.o_cnt = m.o_box + 48 * P;
-        int64_t o = m.o_cnt + 8 * P;
+        int64_t o = m.o_cnt + 16 * P;
         for (int k = 0; k < 2; ++k) { m.o_ids[k] = o; o += 4 * P * S; }
         o = (o + 255) / 256 * 256;
         for (int k = 0; k < 2; ++k) { m.o_snap[k] = o; o += 4 * esz * P * S; }

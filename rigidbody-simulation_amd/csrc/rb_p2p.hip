@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
 //   insert: block 0 reduces the own cell bounds the step kernel folded and
 //           stores them, tagged e + 1, into every peer's mailbox (for the
 //           peers' next pushes), stores push_cnt[q], tagged e, into peer q's
-//           mailbox and resets it, and hands e to the next step kernel
+//           count word of parity e & 1 and resets it, and hands e to the next step kernel
 //           (halo_e); every block waits for all peers' counts of step e,
 //           then the grid copies the received snapshots (inbox parity e & 1)
 //           into the next snapshot buffer and inserts them into the next
@@ -113,10 +113,13 @@ __global__ __launch_bounds__(256) void p2p_exchange_kernel(P2PParams<T> p) {
 //   prime:  before a run's first step, the bounds of the current positions,
 //           tagged (steps taken) + 1, and halo_e, as an insert kernel of the
 //           step before would have left them.
-// A peer pushes into this rank's inbox of parity e & 1 again only at step
-// e + 2, after this rank's bounds of step e + 1 reached it — published by
-// this rank's insert kernel of step e + 1, after its insert of step e
-// finished reading: two inboxes (by parity) suffice.
+// Publishing the bounds at the start of the insert lets a peer run one step
+// ahead: its step e + 1 may push, and its insert e + 1 publish its count,
+// while this rank's insert e still reads.  So the inboxes and the count
+// words alternate by step parity: a peer writes this rank's parity e & 1
+// again only at step e + 2, after this rank's bounds of step e + 1 reached
+// it — published by this rank's insert kernel of step e + 1, after its
+// insert of step e finished reading.
 // Why exact: rb_halo.hpp halo_push.
 
 // One lane per peer (lanes 0..63 of the block) waits until word(q) of every
@@ -176,14 +179,16 @@ __global__ __launch_bounds__(256) void halo_insert_kernel(HaloParams<T> p) {
         for (int d = 0; d < 3; ++d) { r[d] = INT32_MAX; r[3 + d] = INT32_MIN; }
         publish_bounds(p, b, e + 1);
         if (tid < p.P && tid != p.rank) {
+            // counts by step parity: a peer may reach its next insert (and
+            // publish that step's count) while this rank still reads this one
             const int32_t n = p.push_cnt[tid];
-            int64_t *cnt = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_cnt) + p.rank;
+            int64_t *cnt = reinterpret_cast<int64_t *>(p.peer_mail[tid] + L.o_cnt) + (e & 1) * p.P + p.rank;
             store_sys(cnt, (int64_t)pack_epoch(e, n < p.S ? n : (int32_t)p.S));
             p.push_cnt[tid] = 0;
         }
         if (tid == 0) *p.halo_e = e;
     }
-    const int64_t *cnt_in = reinterpret_cast<const int64_t *>(p.mail + L.o_cnt);
+    const int64_t *cnt_in = reinterpret_cast<const int64_t *>(p.mail + L.o_cnt) + (e & 1) * p.P;
     wait_peers(p.P, p.rank, e, p.timeout_ticks, p.ins.err,
                [&](int q) { return (int64_t)((uint64_t)load_sys(cnt_in + q) >> 32); });
     if (tid == 0) {

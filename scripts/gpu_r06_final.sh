@@ -10,6 +10,13 @@ OUT=gpurun_out/final6
 mkdir -p $OUT
 export TMPDIR=/tmp
 step() { echo "== $*  ($(date +%T))"; }
+if [ "${RUN_SUITE:-0}" = 1 ]; then
+  step gpu-suite
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_suite.log 2>&1
+  rc=$?
+  tail -2 $OUT/gpu_suite.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+fi
 if [ "${SKIP_PMC:-0}" != 1 ]; then
   for cp in ${PMC_SHAPES:-"c3 f64 1" "c2 f64 1" "c4 f64 1" "c5 f64 1" "c3 f32 1" "c3 f64 2" "c3 f64 4" "c3 f64 8" "c4 f64 8"}; do
     set -- $cp
@@ -17,8 +24,8 @@ if [ "${SKIP_PMC:-0}" != 1 ]; then
     timeout -k 10 900 python -u profiles/collect_pmc.py $1 $2 $3 > $OUT/pmc_$1_$2_p$3.log 2>&1 || { tail -20 $OUT/pmc_$1_$2_p$3.log; exit 1; }
     tail -2 $OUT/pmc_$1_$2_p$3.log
   done
-  step pmc c3 f64 tile
-  RBHIP_TILE=1 timeout -k 10 900 python -u profiles/collect_pmc.py c3 f64 1 _tile > $OUT/pmc_c3_f64_tile.log 2>&1 || { tail -20 $OUT/pmc_c3_f64_tile.log; exit 1; }
+  [ "${SKIP_TILE_PMC:-0}" != 1 ] && step pmc c3 f64 tile
+  [ "${SKIP_TILE_PMC:-0}" != 1 ] && RBHIP_TILE=1 timeout -k 10 900 python -u profiles/collect_pmc.py c3 f64 1 _tile > $OUT/pmc_c3_f64_tile.log 2>&1 || { tail -20 $OUT/pmc_c3_f64_tile.log; exit 1; }
   cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
 fi
 if [ "${SKIP_BENCH:-0}" != 1 ]; then
