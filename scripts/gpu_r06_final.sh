@@ -18,14 +18,18 @@ if [ "${RUN_SUITE:-0}" = 1 ]; then
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 if [ "${SKIP_PMC:-0}" != 1 ]; then
-  for cp in ${PMC_SHAPES:-"c3 f64 1" "c2 f64 1" "c4 f64 1" "c5 f64 1" "c3 f32 1" "c3 f64 2" "c3 f64 4" "c3 f64 8" "c4 f64 8"}; do
+  # PMC_SHAPES: "cfg dtype P" entries separated by "|"
+  IFS='|' read -r -a shapes <<< "${PMC_SHAPES:-c3 f64 1|c2 f64 1|c4 f64 1|c5 f64 1|c3 f32 1|c3 f64 2|c3 f64 4|c3 f64 8|c4 f64 8}"
+  for cp in "${shapes[@]}"; do
     set -- $cp
     step pmc $1 $2 P=$3
     timeout -k 10 900 python -u profiles/collect_pmc.py $1 $2 $3 > $OUT/pmc_$1_$2_p$3.log 2>&1 || { tail -20 $OUT/pmc_$1_$2_p$3.log; exit 1; }
     tail -2 $OUT/pmc_$1_$2_p$3.log
   done
-  [ "${SKIP_TILE_PMC:-0}" != 1 ] && step pmc c3 f64 tile
-  [ "${SKIP_TILE_PMC:-0}" != 1 ] && RBHIP_TILE=1 timeout -k 10 900 python -u profiles/collect_pmc.py c3 f64 1 _tile > $OUT/pmc_c3_f64_tile.log 2>&1 || { tail -20 $OUT/pmc_c3_f64_tile.log; exit 1; }
+  if [ "${SKIP_TILE_PMC:-0}" != 1 ]; then
+    step pmc c3 f64 tile
+    RBHIP_TILE=1 timeout -k 10 900 python -u profiles/collect_pmc.py c3 f64 1 _tile > $OUT/pmc_c3_f64_tile.log 2>&1 || { tail -20 $OUT/pmc_c3_f64_tile.log; exit 1; }
+  fi
   cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
 fi
 if [ "${SKIP_BENCH:-0}" != 1 ]; then
