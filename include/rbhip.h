@@ -321,7 +321,7 @@ int rb_kernel_timing(rb_world *w, int enable, double *avg_ms, int64_t *launches)
 /* Retired (kept for ABI compatibility with librbhip 0.2): the round-3 tile
  * blocks' configuration.  mode -1 (auto) and 0 (off) are accepted and do
  * nothing; mode 1 returns RB_EUNSUPPORTED.  The step forms are chosen by the
- * library (RB_STAT_FORM); RBHIP_TILE / RBHIP_RESIDENT select them for tests. */
+ * library (RB_STAT_FORM); RBHIP_TILE selects the tile form for tests. */
 int rb_tile_config(rb_world *w, int32_t mode, int32_t kmax, double band, int64_t owned);
 
 #ifdef __cplusplus

@@ -74,7 +74,7 @@ with rbhip.World(sc) as w:
     w.shard_run(K); torch.cuda.synchronize()
     print("shard_run (p2p, 1 rk)  host %.2f us/step  device %.2f us/step" % timed(lambda: w.shard_run(K)))
 
-# the peer-to-peer halo exchange with one rank: step kernel + push kernel +
+# the peer-to-peer halo exchange with one rank: step kernel (with the push) +
 # insert kernel, no peers (the fixed cost a halo step adds)
 with rbhip.World(sc) as w:
     w.set_stream(torch.cuda.current_stream().cuda_stream)
