@@ -6,9 +6,9 @@
 # processes time-slice one GPU).  Then the one-rank loop costs.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/rehearse6
+OUT=${OUT:-gpurun_out/rehearse6}
 mkdir -p $OUT
-for spec in "2 c3" "8 c3" "8 c4"; do
+for spec in ${SPECS:-"2 c3" "4 c3" "8 c3" "8 c4"}; do
   set -- $spec
   echo "== rehearse $1 $2 ($(date +%T))"
   RBHIP_BENCH_BACKEND=gloo RBHIP_SHARD_TRANSPORT=p2p timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
