@@ -20,9 +20,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--K", type=int, default=20)
     ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--lib", default=None)
     a = ap.parse_args()
     import torch
     torch.cuda.init()
+    from rbhip import _lib
+    if a.lib:
+        _lib.load(a.lib)
     import rbhip
     from rbhip import scenes
     with rbhip.World(scenes.make("c3")) as w:
@@ -46,7 +50,7 @@ def main():
             t5 = time.perf_counter()
             rows.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t5 - t0, e0.elapsed_time(e1) * 1e-3))
         med = [statistics.median(r[k] for r in rows) * 1e6 for k in range(7)]
-        print(f"K={a.K} graph_min={os.environ.get('RBHIP_GRAPH_MIN_STEPS', 'default')}: median us: ev0.record {med[0]:.1f}, rb_step_async {med[1]:.1f}, ev1.record {med[2]:.1f}, "
+        print(f"{os.path.basename(a.lib or 'librbhip.so')} K={a.K} graph_min={os.environ.get('RBHIP_GRAPH_MIN_STEPS', 'default')}: median us: ev0.record {med[0]:.1f}, rb_step_async {med[1]:.1f}, ev1.record {med[2]:.1f}, "
               f"rb_sync {med[3]:.1f}, torch sync {med[4]:.1f}; wall {med[5]:.1f} ({med[5] / a.K:.2f} per step), "
               f"events {med[6]:.1f} ({med[6] / a.K:.2f} per step)", flush=True)
 
